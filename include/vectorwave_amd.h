@@ -1,0 +1,220 @@
+/*
+ * vectorwave_amd.h -- C ABI of the MI355X (gfx950) MODWT / SWT engine.
+ *
+ * Drop-in boundary for VectorWave's MODWT/SWT hot path: the per-level a-trous
+ * low/high-pass convolutions (forward and inverse, PERIODIC / ZERO_PADDING /
+ * SYMMETRIC).  Plain C types only -- no torch, no HIP types in signatures --
+ * so a JNI (or Java 22+ FFM) shim, ctypes, or C/C++ host code can bind it.
+ *
+ * Reference interfaces each entry point replaces (paths relative to
+ * /root/reference, prefixes core/ = vectorwave-core/src/main/java/com/morphiqlabs/wavelet/,
+ * ext/ = vectorwave-extensions/src/main/java/com/morphiqlabs/wavelet/):
+ *
+ *   vw_modwt_forward_*      MultiLevelMODWTTransform.decompose / decomposeMutable
+ *                             core/modwt/MultiLevelMODWTTransform.java:209-330
+ *                           BatchMODWT.multiLevelAoS  ext/extensions/modwt/BatchMODWT.java:90-111
+ *                           BatchSIMDMODWT.batchMultiLevelMODWTSoA  ext/extensions/modwt/BatchSIMDMODWT.java:343-424
+ *                           VectorWaveSwtAdapter.forward  core/swt/VectorWaveSwtAdapter.java:198-394
+ *   vw_modwt_inverse_*      MultiLevelMODWTTransform.reconstruct / reconstructFromLevel / reconstructLevels
+ *                             core/modwt/MultiLevelMODWTTransform.java:339-446, :554-645
+ *                           BatchMODWT.inverseMultiLevelAoS  ext/extensions/modwt/BatchMODWT.java:151-178
+ *                           VectorWaveSwtAdapter.inverse / extractLevel  core/swt/VectorWaveSwtAdapter.java:435-487, :576-598
+ *   vw_modwt1_forward_*     MODWTTransform.forward / forwardBatch  core/modwt/MODWTTransform.java:131-189, :486-614
+ *                           BatchMODWT.singleLevelAoS  ext/extensions/modwt/BatchMODWT.java:62-79
+ *   vw_modwt1_inverse_*     MODWTTransform.inverse / inverseBatch  core/modwt/MODWTTransform.java:203-299, :531-689
+ *                           BatchMODWT.inverseSingleLevelAoS  ext/extensions/modwt/BatchMODWT.java:122-139
+ *   vw_swt_denoise_*        VectorWaveSwtAdapter.denoise  core/swt/VectorWaveSwtAdapter.java:532-562
+ *   vw_noise_sigma_*        VectorWaveSwtAdapter.estimateNoiseSigma  core/swt/VectorWaveSwtAdapter.java:627-645
+ *   vw_threshold_*          MutableMultiLevelMODWTResult.applyThreshold  core/modwt/MutableMultiLevelMODWTResult.java:83-114
+ *   vw_stream_*             BatchStreamingMODWT  ext/extensions/modwt/BatchStreamingMODWT.java:55-275
+ *   vw_max_levels           MultiLevelMODWTTransform.getMaximumLevels  core/modwt/MultiLevelMODWTTransform.java:455-501, :693-695
+ *   status codes            core/exception/ErrorCode.java:24-118 (see the table below)
+ *
+ * Memory: by default every array argument is a DEVICE pointer (hipMalloc /
+ * torch CUDA storage) on the context's device, and work is enqueued on the
+ * context's stream (the call returns after enqueueing unless VW_FLAG_SYNC or
+ * validation needs a result).  With VW_FLAG_HOST_MEMORY all arrays are host
+ * pointers: the engine stages them through its own device workspace and the
+ * call is synchronous (the JNI/FFM path).  Filter taps (lo/hi) are always host
+ * pointers of L doubles: the caller passes wavelet.lowPassDecomposition() /
+ * highPassDecomposition() (== reconstruction filters for orthogonal
+ * wavelets), exactly as the reference reads them.
+ *
+ * Layout: x[B][ldx] row-major (row b at x + b*ldx, ldx >= N), details
+ * [J][B][N] (level 1 = finest first; BatchMODWT's detailPerLevel order),
+ * approx [B][N], y [B][N].
+ *
+ * Threading: one vw_ctx per device; a context may be used from several host
+ * threads, calls are serialized on its stream.  The engine retains no caller
+ * buffer after a call returns.
+ */
+#ifndef VECTORWAVE_AMD_H
+#define VECTORWAVE_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VW_API __attribute__((visibility("default")))
+
+typedef struct vw_ctx vw_ctx;
+typedef struct vw_stream vw_stream;
+typedef int vw_status;
+
+/* Status codes.  Reference ErrorCode (core/exception/ErrorCode.java) -> status. */
+enum {
+    VW_OK = 0,
+    VW_ERR_NULL = 1,          /* NullPointerException                         */
+    VW_ERR_EMPTY = 2,         /* VAL_006 VAL_EMPTY (empty signal / batch)     */
+    VW_ERR_NONFINITE = 3,     /* VAL_003 VAL_NON_FINITE_VALUES; index via vw_last_error_index() */
+    VW_ERR_LEVEL = 4,         /* CFG_004 CFG_INVALID_DECOMPOSITION_LEVEL      */
+    VW_ERR_TOO_LARGE = 5,     /* VAL_005 VAL_TOO_LARGE (L_j > N)              */
+    VW_ERR_BOUNDARY = 6,      /* CFG_003 CFG_UNSUPPORTED_BOUNDARY_MODE        */
+    VW_ERR_ARG = 7,           /* IllegalArgumentException (shapes, ld, taps)  */
+    VW_ERR_DEVICE = 8,        /* HIP runtime failure                          */
+    VW_ERR_UNSUPPORTED = 9,   /* UnsupportedOperationException                */
+    VW_ERR_STATE = 10         /* IllegalStateException (streaming)            */
+};
+
+/* BoundaryMode (core/api/BoundaryMode.java:20-50); CONSTANT is not a MODWT mode. */
+enum { VW_PERIODIC = 0, VW_SYMMETRIC = 1, VW_ZERO_PADDING = 2 };
+
+/* Wavelet identity for SymmetricAlignmentStrategy.decide, which compares
+ * object identity (core/modwt/SymmetricAlignmentStrategy.java:65-96).
+ * VW_WID_OTHER means "decide by filter length" (Haar if L <= 2, the L >= 12
+ * rule, else the DB4 rule). */
+enum {
+    VW_WID_OTHER = 0, VW_WID_HAAR = 1, VW_WID_DB2 = 2, VW_WID_DB4 = 4, VW_WID_DB6 = 6,
+    VW_WID_DB8 = 8, VW_WID_DB10 = 10, VW_WID_SYM4 = 104, VW_WID_SYM8 = 108,
+    VW_WID_COIF1 = 201, VW_WID_COIF2 = 202, VW_WID_COIF3 = 203, VW_WID_COIF5 = 205
+};
+
+/* Semantics flags (OR-able). */
+enum {
+    /* MultiLevelMODWTTransform / SWT semantics: level cap 9 (calculateMaxLevels) and the
+     * L_j > N guard.  Without it: BatchMODWT semantics (no cap, levels >= 1). */
+    VW_FLAG_CORE_LEVELS = 1u << 0,
+    /* Non-finite input check (ValidationUtils.validateFiniteValues) and result re-validation
+     * (MODWTResultImpl ctor) -> VW_ERR_NONFINITE.  Fused into the kernels. */
+    VW_FLAG_VALIDATE = 1u << 1,
+    /* MultiLevelMODWTTransform.decompose PERIODIC dispatch: levels with N >= 1024 and
+     * N/8 < L_j <= N/2 use WaveletOperations' FFT path, which zero-pads to nextPow2(N)
+     * (core/modwt/MultiLevelMODWTTransform.java:734-742, core/util/FftHeuristics.java:30-34).
+     * The engine computes that linear-over-nextPow2 convolution directly (no FFT). */
+    VW_FLAG_FFT_SWITCH = 1u << 2,
+    /* Fused multiply-add accumulation (faster; differs from the Java order by ~1 ulp per tap).
+     * Default (flag clear) is EXACT: separate multiply and add in the reference's order,
+     * bit-identical to vectorwave-core. */
+    VW_FLAG_FMA = 1u << 3,
+    /* All array arguments are host pointers (staged through the context workspace). */
+    VW_FLAG_HOST_MEMORY = 1u << 4,
+    /* Synchronize the context stream before returning. */
+    VW_FLAG_SYNC = 1u << 5,
+    /* Single-level inverse, SYMMETRIC: use MODWTTransform.inverseBatchOptimized's (t+l)
+     * orientation (core/modwt/MODWTTransform.java:671-684) instead of inverse's (t-l). */
+    VW_FLAG_BATCH_SYM_INVERSE = 1u << 6,
+    /* Single-level forward: BatchSIMDMODWT.haarBatchMODWTSoA's hard-coded 0.5/-0.5 taps
+     * (ext/extensions/modwt/BatchSIMDMODWT.java:86-140) when L == 2. */
+    VW_FLAG_BATCH_HAAR = 1u << 7
+};
+
+/* ---- context ---------------------------------------------------------- */
+VW_API vw_status vw_ctx_create(int device, vw_ctx **out);
+VW_API vw_status vw_ctx_destroy(vw_ctx *ctx);
+/* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
+VW_API vw_status vw_ctx_set_stream(vw_ctx *ctx, void *hip_stream);
+VW_API void *vw_ctx_get_stream(vw_ctx *ctx);
+VW_API vw_status vw_ctx_synchronize(vw_ctx *ctx);
+VW_API int vw_ctx_device(vw_ctx *ctx);
+
+/* Thread-local message / index of the last failing call on this thread. */
+VW_API const char *vw_last_error(void);
+VW_API int64_t vw_last_error_index(void);
+VW_API const char *vw_version(void);
+
+/* ---- bookkeeping (host only) ------------------------------------------ */
+/* getMaximumLevels(N) for a base filter of length L: largest J <= 9 with (L-1)*2^(J-1)+1 <= N. */
+VW_API int vw_max_levels(int64_t N, int L);
+/* (L-1)*2^(level-1)+1 */
+VW_API int64_t vw_upsampled_length(int L, int level);
+
+/* ---- multi-level MODWT ------------------------------------------------- */
+VW_API vw_status vw_modwt_forward_f64(vw_ctx *ctx, const double *x, int64_t B, int64_t N, int64_t ldx,
+                                      const double *lo, const double *hi, int L, int wavelet_id,
+                                      int boundary, int J, unsigned flags,
+                                      double *details, double *approx);
+VW_API vw_status vw_modwt_forward_f32(vw_ctx *ctx, const float *x, int64_t B, int64_t N, int64_t ldx,
+                                      const double *lo, const double *hi, int L, int wavelet_id,
+                                      int boundary, int J, unsigned flags,
+                                      float *details, float *approx);
+
+/* detail_mask bit (j-1) set = use d_j, clear = zero details at level j
+ * (reconstructFromLevel / reconstructLevels / extractLevel); approx_zero = 1 starts from a
+ * zero approximation.  details may be NULL when detail_mask == 0; approx may be NULL when
+ * approx_zero == 1.  Plain reconstruct: detail_mask = ~0u, approx_zero = 0. */
+VW_API vw_status vw_modwt_inverse_f64(vw_ctx *ctx, const double *details, const double *approx,
+                                      int64_t B, int64_t N, const double *lo, const double *hi, int L,
+                                      int wavelet_id, int boundary, int J, unsigned detail_mask,
+                                      int approx_zero, unsigned flags, double *y);
+VW_API vw_status vw_modwt_inverse_f32(vw_ctx *ctx, const float *details, const float *approx,
+                                      int64_t B, int64_t N, const double *lo, const double *hi, int L,
+                                      int wavelet_id, int boundary, int J, unsigned detail_mask,
+                                      int approx_zero, unsigned flags, float *y);
+
+/* ---- single-level MODWT (MODWTTransform: pairwise inverse sums, any N >= 1) --- */
+VW_API vw_status vw_modwt1_forward_f64(vw_ctx *ctx, const double *x, int64_t B, int64_t N, int64_t ldx,
+                                       const double *lo, const double *hi, int L, int boundary,
+                                       unsigned flags, double *approx, double *detail);
+VW_API vw_status vw_modwt1_inverse_f64(vw_ctx *ctx, const double *approx, const double *detail,
+                                       int64_t B, int64_t N, const double *lo, const double *hi, int L,
+                                       int boundary, unsigned flags, double *y);
+
+/* ---- SWT denoise -------------------------------------------------------- */
+/* threshold < 0: universal threshold sigma*sqrt(2 ln N), sigma = median(|d_1|)/0.6745 per signal;
+ * threshold >= 0: that value on every detail level.  soft: 1 soft, 0 hard.
+ * thresholds_out (optional, [B], same memory kind as y) receives the threshold used per signal. */
+VW_API vw_status vw_swt_denoise_f64(vw_ctx *ctx, const double *x, int64_t B, int64_t N, int64_t ldx,
+                                    const double *lo, const double *hi, int L, int wavelet_id,
+                                    int boundary, int J, double threshold, int soft, unsigned flags,
+                                    double *y, double *thresholds_out);
+/* sigma[b] = median(|coeffs[b][:]|) / 0.6745 (exact selection, even N = mean of middle pair). */
+VW_API vw_status vw_noise_sigma_f64(vw_ctx *ctx, const double *coeffs, int64_t B, int64_t N,
+                                    unsigned flags, double *sigma);
+/* In-place soft/hard threshold of c[B][N] with per-signal thresholds thr[B] (device or host per flags). */
+VW_API vw_status vw_threshold_f64(vw_ctx *ctx, double *c, int64_t B, int64_t N, const double *thr,
+                                  int soft, unsigned flags);
+
+/* ---- streaming (BatchStreamingMODWT) ------------------------------------ */
+/* levels >= 1.  PERIODIC: every block independent (== vw_modwt_forward, no cap).
+ * ZERO_PADDING / SYMMETRIC: per-level left history of L_j - 1 samples kept on the device. */
+VW_API vw_status vw_stream_create(vw_ctx *ctx, const double *lo, const double *hi, int L,
+                                  int boundary, int levels, vw_stream **out);
+VW_API vw_status vw_stream_destroy(vw_stream *s);
+/* block [B][n] -> details [levels][B][n], approx [B][n] (f64). */
+VW_API vw_status vw_stream_process_f64(vw_stream *s, const double *block, int64_t B, int64_t n,
+                                       unsigned flags, double *details, double *approx);
+/* Synthetic tail of tail_len samples (ZERO/SYMMETRIC only); tail_len <= min history length. */
+VW_API vw_status vw_stream_flush_f64(vw_stream *s, int64_t tail_len, unsigned flags,
+                                     double *details, double *approx);
+VW_API int64_t vw_stream_history_length(vw_stream *s, int level);
+
+/* ---- device utilities ---------------------------------------------------- */
+/* x[i] = 2*u - 1 with u = (splitmix64(seed ^ (offset + i)) >> 11) * 2^-53. */
+VW_API vw_status vw_fill_uniform_f64(vw_ctx *ctx, double *x, int64_t count, uint64_t seed, int64_t offset);
+VW_API vw_status vw_fill_uniform_f32(vw_ctx *ctx, float *x, int64_t count, uint64_t seed, int64_t offset);
+VW_API vw_status vw_device_alloc(vw_ctx *ctx, int64_t bytes, void **out);
+VW_API vw_status vw_device_free(vw_ctx *ctx, void *p);
+VW_API vw_status vw_memcpy(vw_ctx *ctx, void *dst, const void *src, int64_t bytes, int kind /*0 H2D,1 D2H,2 D2D*/);
+
+/* Timing: average duration (ms) of the last `count` launches of the dominant kernel family
+ * recorded with HIP events on the context stream when profiling is enabled. */
+VW_API vw_status vw_ctx_enable_timing(vw_ctx *ctx, int enable);
+VW_API vw_status vw_ctx_kernel_time(vw_ctx *ctx, const char *family, double *total_ms, int64_t *launches);
+VW_API vw_status vw_ctx_reset_timing(vw_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VECTORWAVE_AMD_H */

@@ -1,0 +1,301 @@
+"""Pins the CPU restatement (oracle/) to the reference's own tests, known answers and fixtures.
+
+Each test names the JUnit test it restates (paths under /root/reference; the reference cannot run
+here -- no JDK -- so its assertions and inputs are carried over as data).
+"""
+import math
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from vectorwave_amd.wavelets import Coiflet, Daubechies, Haar, Symlet, WID_COIF2, WID_DB4, WID_HAAR, WID_SYM4
+
+H = Haar.INSTANCE
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def composite_sin(n, seed=7, noise=0.0):
+    """TestSignals.compositeSin (ctest/testing/TestSignals.java:18-30) with noiseStd = 0."""
+    t = np.arange(n) / float(n)
+    return (np.sin(2 * math.pi * 2 * t) + 0.5 * np.sin(2 * math.pi * 7 * t) + 0.25 * np.cos(2 * math.pi * 13 * t))
+
+
+# ---- known answers --------------------------------------------------------------------------------
+def test_pw_circular_convolution_known_answer():
+    # ctest/modwt/MODWTPercivalWaldenValidationTest.java:38-83
+    s = 1.0 / math.sqrt(2.0)
+    f = [H.lowPassDecomposition()[0] * s, H.lowPassDecomposition()[1] * s]
+    out = O.conv("circular", [1.0, 2.0, 3.0, 4.0], f)
+    np.testing.assert_allclose(out, [2.5, 1.5, 2.5, 3.5], atol=1e-10)
+
+
+def test_time_reversed_filter_known_answer():
+    # etest/modwt/TimeReversedFilterTest.java:22-49: W_0 = h*X_0 + h*X_7, W_1 = h*X_1 + h*X_0
+    h = 0.7071067811865475
+    out = O.conv("circular", np.arange(1.0, 9.0), [h, h])
+    assert out[0] == h * 1 + h * 8
+    assert out[1] == h * 2 + h * 1
+
+
+def test_pw_formula_restated_complete_transform():
+    # MODWTPercivalWaldenValidationTest.java:89-134 (expected recomputed with P&W's formula)
+    x = np.array([1.0, 2.0, 3.0, 4.0])
+    a, d = O.modwt_forward(x, H.lowPassDecomposition(), H.highPassDecomposition(), O.PERIODIC)
+    s = 1.0 / math.sqrt(2.0)
+    lo = [v * s for v in H.lowPassDecomposition()]
+    hi = [v * s for v in H.highPassDecomposition()]
+    ea = [sum(lo[l] * x[(t - l + 4) % 4] for l in range(2)) for t in range(4)]
+    ed = [sum(hi[l] * x[(t - l + 4) % 4] for l in range(2)) for t in range(4)]
+    np.testing.assert_allclose(a, ea, atol=1e-10)
+    np.testing.assert_allclose(d, ed, atol=1e-10)
+
+
+@pytest.mark.parametrize("x", [[1.0, 2.0, 3.0, 4.0], [5.0, 5.0, 5.0, 5.0], [1.0, -1.0, 1.0, -1.0],
+                               [2.5, 1.7, 8.3, -4.2], [0.0, 0.0, 1.0, 0.0]])
+def test_pw_perfect_reconstruction(x):
+    # MODWTPercivalWaldenValidationTest.java:139-165
+    a, d = O.modwt_forward(x, H.lowPassDecomposition(), H.highPassDecomposition(), O.PERIODIC)
+    y = O.modwt_inverse(a, d, H.lowPassReconstruction(), H.highPassReconstruction(), O.PERIODIC)
+    np.testing.assert_allclose(y, x, atol=1e-10)
+
+
+def test_energy_conservation():
+    # MODWTPercivalWaldenValidationTest.java:171-195
+    x = np.array([3.2, -1.7, 4.5, 2.1, -0.8, 5.3, 1.9, -2.4])
+    a, d = O.modwt_forward(x, H.lowPassDecomposition(), H.highPassDecomposition(), O.PERIODIC)
+    assert abs(float(x @ x) - float(a @ a + d @ d)) < 1e-10
+
+
+def test_shift_equivariance():
+    # TimeReversedFilterTest.java:57-89
+    a, _ = O.modwt_forward([1, 2, 3, 4], H.lowPassDecomposition(), H.highPassDecomposition(), O.PERIODIC)
+    b, _ = O.modwt_forward([2, 3, 4, 1], H.lowPassDecomposition(), H.highPassDecomposition(), O.PERIODIC)
+    np.testing.assert_allclose(b, np.roll(a, -1), atol=1e-10)
+
+
+# ---- bookkeeping ------------------------------------------------------------------------------------
+@pytest.mark.parametrize("n,L,expect", [(1024, 2, 9), (4096, 8, 9), (65536, 16, 9), (8, 8, 0), (7, 8, 0),
+                                        (100, 8, 4), (512, 8, 7), (129, 2, 8), (16384, 16, 9), (8192, 30, 9)])
+def test_max_levels(n, L, expect):
+    # MultiLevelMODWTTransform.calculateMaxLevels :455-501 (loop bound 10 -> cap 9)
+    assert O.max_levels(n, L) == expect
+
+
+def test_upsample_scale_layout():
+    # ScalarOps.upsampleAndScaleForIMODWTSynthesis :909-916
+    f = O.upsample_scale(Daubechies.DB4.lowPassDecomposition(), 3)
+    assert len(f) == 7 * 4 + 1
+    s = 1.0 / math.sqrt(2.0)
+    for i, h in enumerate(Daubechies.DB4.lowPassDecomposition()):
+        assert f[4 * i] == h * s
+    assert np.count_nonzero(f) == 8
+
+
+@pytest.mark.parametrize("idx,n,expect", [(-1, 4, 0), (-2, 4, 1), (4, 4, 3), (5, 4, 2), (-9, 4, 0), (8, 4, 0),
+                                          (-5, 4, 3), (11, 4, 3), (2, 4, 2)])
+def test_symmetric_index(idx, n, expect):
+    # MathUtils.symmetricBoundaryExtension :30-51 ("... b a | a b c d | d c b a ...")
+    assert O.symmetric_index(idx, n) == expect
+
+
+def test_sym_alignment_tables():
+    # SymmetricAlignmentStrategy.decide :43-117
+    assert O.sym_decide(WID_HAAR, 2, 1) == (1, 0, 1, 0)
+    assert O.sym_decide(WID_HAAR, 2, 3) == (1, -1, 1, 0)
+    assert O.sym_decide(WID_DB4, 8, 2) == (0, -1, 1, 0)
+    assert O.sym_decide(WID_SYM4, 8, 4) == (1, 0, 0, 0)
+    assert O.sym_decide(WID_COIF2, 12, 2) == (1, 1, 0, 0)
+    assert O.sym_decide(0, 16, 3) == (0, -1, 1, -1)
+    assert O.sym_decide(0, 16, 4) == (0, 0, 1, 0)
+
+
+# ---- round trips ---------------------------------------------------------------------------------
+@pytest.mark.parametrize("w,eps", [(H, 1e-9), (Daubechies.DB4, 1e-9), (Symlet.SYM4, 1e-6), (Coiflet.COIF2, 5e-4)])
+def test_multilevel_round_trip_and_energy(w, eps):
+    # ctest/modwt/MultiLevelModwtCorrectnessTest.java:27-72 (N=512, J=min(5,max))
+    n = 512
+    x = composite_sin(n)
+    J = min(5, O.max_levels(n, len(w.lowPassDecomposition())))
+    det, app = O.decompose(x, w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC, J)
+    y = O.reconstruct(det, app, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC)
+    assert np.max(np.abs(x - y)) < eps
+    tot = float(app @ app) + sum(float(d @ d) for d in det)
+    tol = {1e-9: 1e-8, 1e-6: 1e-6, 5e-4: 5e-4}[eps]
+    assert abs(tot - float(x @ x)) <= tol * float(x @ x)
+
+
+@pytest.mark.parametrize("n", [128, 129, 256])
+@pytest.mark.parametrize("w", [H, Daubechies.DB4])
+def test_periodic_round_trip_single_and_multi(n, w):
+    # ctest/modwt/ModwtPeriodicRoundTripTest.java:121-139 (PR < 1e-9)
+    x = O.java_random_signal(n, 42)
+    a, d = O.modwt_forward(x, w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC)
+    y = O.modwt_inverse(a, d, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC)
+    assert np.max(np.abs(x - y)) < 1e-9
+    J = min(4, O.max_levels(n, len(w.lowPassDecomposition())))
+    det, app = O.decompose(x, w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC, J)
+    y = O.reconstruct(det, app, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC)
+    assert np.max(np.abs(x - y)) < 1e-9
+
+
+def test_haar_1m_max_levels_round_trip():
+    # ctest/modwt/MultiLevelMODWTOverflowTest.java:99-125 (1M samples, max levels, PR < 1e-10); 64K here
+    n = 1 << 16
+    x = O.java_random_signal(n, 5)
+    J = O.max_levels(n, 2)
+    det, app = O.decompose(x, H.lowPassDecomposition(), H.highPassDecomposition(), O.PERIODIC, J)
+    y = O.reconstruct(det, app, H.lowPassReconstruction(), H.highPassReconstruction(), O.PERIODIC)
+    assert np.max(np.abs(x - y)) < 1e-10
+
+
+# ---- cross-implementation parity ------------------------------------------------------------------
+def test_fft_vs_scalar_parity_random():
+    # ctest/internal/ScalarOpsFftParityTest.java:19-45 (tol ToleranceConstants.FFT_PARITY_TOLERANCE = 1e-11)
+    rnd = O.JavaRandom(42)
+    for n in (2048, 4096):
+        x = np.array([rnd.nextDouble() * 2 - 1 for _ in range(n)])
+        L = max(8, n // 4)
+        f = np.array([rnd.nextDouble() * 2 - 1 for _ in range(L)])
+        np.testing.assert_allclose(O.conv("fft", x, f), O.conv("circular", x, f), rtol=0, atol=1e-11)
+
+
+def test_fft_branch_not_circular_for_non_pow2():
+    # N not a power of two -> zero-padded to nextPow2, first L-1 outputs differ
+    n, rnd = 1500, O.JavaRandom(3)
+    x = np.array([rnd.nextDouble() * 2 - 1 for _ in range(n)])
+    f = O.upsample_scale(Daubechies.DB4.lowPassDecomposition(), 6)  # L_j = 225 > N/8
+    assert O.conv("fft", x, f)[0] != pytest.approx(O.conv("circular", x, f)[0], abs=1e-6)
+    # restated exactly: circular over m = nextPow2(N) with zeros beyond N
+    m = 2048
+    xp = np.zeros(m)
+    xp[:n] = x
+    lin = np.array([sum(f[l] * xp[(t - l) % m] for l in range(len(f))) for t in range(40)])
+    np.testing.assert_allclose(O.conv("fft", x, f)[:40], lin, atol=1e-12)
+
+
+def test_swt_matches_modwt():
+    # ctest/swt/SwtAdapterParityTest.java:28-56 (1e-10); the restatements agree bit for bit
+    x = O.java_random_signal(1024, 11)
+    w = Daubechies.DB4
+    d1, a1 = O.decompose(x, w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC, 4)
+    d2, a2 = O.swt_forward(x, w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC, 4)
+    assert np.array_equal(d1, d2) and np.array_equal(a1, a2)
+    y1 = O.reconstruct(d1, a1, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC)
+    y2 = O.swt_reconstruct_periodic(d1, a1, w.lowPassReconstruction(), w.highPassReconstruction())
+    assert np.array_equal(y1, y2)
+
+
+def test_batch_multilevel_matches_core():
+    # etest/modwt/BatchMODWTMultiLevelParityTest.java:17-46 (B=3, N=128, J=3, 1e-10)
+    w = Daubechies.DB4
+    for b in range(3):
+        x = O.java_random_signal(128, 100 + b)
+        d1, a1 = O.decompose(x, w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC, 3, core=True)
+        d2, a2 = O.decompose(x, w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC, 3, core=False)
+        assert np.array_equal(d1, d2) and np.array_equal(a1, a2)
+
+
+def test_batch_single_haar_quirk_within_tolerance():
+    # etest/modwt/BatchMODWTApiTest.java:72-102 (batch SIMD vs core at 1e-10; Haar uses 0.5 taps)
+    x = O.java_random_signal(256, 9)
+    a1, d1 = O.batch_single(x, H.lowPassDecomposition(), H.highPassDecomposition(), True)
+    a2, d2 = O.modwt_forward(x, H.lowPassDecomposition(), H.highPassDecomposition(), O.PERIODIC)
+    np.testing.assert_allclose(a1, a2, atol=1e-10)
+    np.testing.assert_allclose(d1, d2, atol=1e-10)
+
+
+@pytest.mark.parametrize("boundary", [O.ZERO_PADDING, O.SYMMETRIC])
+def test_streaming_history_matches_whole_signal(boundary):
+    # etest/modwt/BatchStreamingMODWTStreamingParityTest.java:45-105: blocks + left history == whole signal
+    w = Daubechies.DB4
+    lo, hi = w.lowPassDecomposition(), w.highPassDecomposition()
+    x = O.java_random_signal(512, 21)
+    f_lo, f_hi = O.upsample_scale(lo, 1), O.upsample_scale(hi, 1)
+    hl = len(f_lo) - 1
+    if boundary == O.ZERO_PADDING:
+        hist = np.zeros(hl)
+        whole_a = O.conv("zero", x, f_lo)
+    else:
+        hist = np.array([x[O.symmetric_index(p - hl, 128)] for p in range(hl)])
+        whole_a = O.conv("symmetric", x, f_lo)
+    outs = []
+    for blk in range(4):
+        xb = x[blk * 128:(blk + 1) * 128]
+        a, _ = O.conv_with_history(hist, xb, f_lo, f_hi)
+        outs.append(a)
+        hist = np.concatenate([hist, xb])[-hl:]
+    got = np.concatenate(outs)
+    if boundary == O.ZERO_PADDING:
+        np.testing.assert_array_equal(got, whole_a)
+    else:  # the first block's left history mirrors the block itself (same as the whole signal)
+        np.testing.assert_array_equal(got, whole_a)
+
+
+# ---- SYMMETRIC NRMSE baseline fixture ----------------------------------------------------------
+def _load_baseline():
+    # vectorwave-core/src/test/resources/baselines/symmetric_nrmse_baseline.properties (copied as data)
+    vals = {}
+    with open(os.path.join(GOLDEN, "symmetric_nrmse_baseline.properties")) as fh:
+        for line in fh:
+            line = line.strip()
+            if not line or line.startswith("#"):
+                continue
+            k, v = line.split("=")
+            vals[tuple(k.split(","))] = float(v)
+    return vals
+
+
+def test_symmetric_nrmse_baseline_guard():
+    # ctest/modwt/SymmetricNRMSEBaselineGuardTest.java:21-97 (interior NRMSE <= 1.1 x baseline)
+    reg = {"haar": (H, WID_HAAR), "db4": (Daubechies.DB4, WID_DB4), "sym4": (Symlet.SYM4, WID_SYM4),
+           "coif2": (Coiflet.COIF2, WID_COIF2)}
+    for (wname, n, level), base in _load_baseline().items():
+        w, wid = reg[wname]
+        n, level = int(n), int(level)
+        x = O.java_random_signal(n, 123)
+        L = len(w.lowPassDecomposition())
+        J = max(1, min(level, O.max_levels(n, L)))
+        det, app = O.decompose(x, w.lowPassDecomposition(), w.highPassDecomposition(), O.SYMMETRIC, J)
+        y = O.reconstruct(det, app, w.lowPassReconstruction(), w.highPassReconstruction(), O.SYMMETRIC, wid)
+        lups = (L - 1) * (1 << max(0, J - 1)) + 1
+        margin = min(n // 4, max(1, lups // 2))
+        s, e = max(0, margin), min(n, n - margin)
+        num = float(np.sum((x[s:e] - y[s:e]) ** 2))
+        den = float(np.sum(x[s:e] ** 2))
+        cur = math.sqrt(num / den)
+        assert cur <= base * 1.10, (wname, n, level, cur, base)
+
+
+# ---- denoise -------------------------------------------------------------------------------------
+def test_noise_sigma_median_even_odd():
+    # VectorWaveSwtAdapter.estimateNoiseSigma :627-645
+    assert O.noise_sigma([1.0, -3.0, 2.0, -4.0]) == ((2.0 + 3.0) / 2.0) / 0.6745
+    assert O.noise_sigma([1.0, -3.0, 2.0]) == 2.0 / 0.6745
+
+
+def test_threshold_soft_hard():
+    # MutableMultiLevelMODWTResult.applyThresholdToArray :97-114
+    c = [-3.0, -1.0, 0.0, 0.5, 2.0, 1.0]
+    assert list(O.threshold(c, 1.0, True)) == [-2.0, 0.0, 0.0, 0.0, 1.0, 0.0]
+    assert list(O.threshold(c, 1.0, False)) == [-3.0, 0.0, 0.0, 0.0, 2.0, 0.0]
+
+
+def test_universal_threshold_denoise_reduces_noise():
+    # SWT denoise path (VectorWaveSwtAdapter.java:532-562) on a noisy composite sinusoid
+    n = 1024
+    clean = composite_sin(n)
+    rnd = np.random.default_rng(0)
+    noisy = clean + 0.2 * rnd.standard_normal(n)
+    w = Symlet.SYM8
+    y, T = O.swt_denoise(noisy, w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC, 4)
+    assert T > 0
+    assert np.sqrt(np.mean((y - clean) ** 2)) < np.sqrt(np.mean((noisy - clean) ** 2))
+
+
+def test_java_random_matches_reference_stream():
+    # java.util.Random(42): first nextDouble values are fixed by the JDK spec (LCG 0x5DEECE66D)
+    r = O.JavaRandom(42)
+    assert r.nextDouble() == 0.7275636800328681
+    assert r.nextDouble() == 0.6832234717598454

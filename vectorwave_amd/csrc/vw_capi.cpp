@@ -1,0 +1,1084 @@
+// vw_capi.cpp -- C ABI of the MI355X MODWT/SWT engine (include/vectorwave_amd.h).
+//
+// Host-side bookkeeping restated from the reference (level cap, L_j guard, symmetric alignment
+// tables, FFT-switch region, status mapping), then one fused HIP launch per transform
+// (vw_kernels.hip), or one tiled launch per level for signals longer than LDS holds.
+#include "../../include/vectorwave_amd.h"
+#include "vw_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+using namespace vw;
+
+// ------------------------------------------------------------------------------------------------
+// Errors (thread-local, like the reference's exceptions are per call site)
+static thread_local std::string t_err;
+static thread_local int64_t t_err_index = -1;
+
+static vw_status fail(vw_status code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  t_err = buf;
+  if (code != VW_ERR_NONFINITE) t_err_index = -1;
+  return code;
+}
+
+static vw_status ok() {
+  t_err.clear();
+  t_err_index = -1;
+  return VW_OK;
+}
+
+#define VW_HIP(call)                                                                         \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess) return fail(VW_ERR_DEVICE, "%s: %s", #call, hipGetErrorString(e_)); \
+  } while (0)
+
+// ------------------------------------------------------------------------------------------------
+struct TimedLaunch {
+  std::string family;
+  hipEvent_t start, stop;
+};
+
+struct vw_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::recursive_mutex mu;
+  void* ws = nullptr;          // tiled-path ping-pong buffers
+  size_t ws_bytes = 0;
+  void* ws2 = nullptr;         // denoise coefficients / thresholds
+  size_t ws2_bytes = 0;
+  unsigned long long* bad = nullptr;   // device word for the fused non-finite check
+  bool timing = false;
+  std::vector<TimedLaunch> pending;
+  std::vector<hipEvent_t> event_pool;
+  std::map<std::string, std::pair<double, int64_t>> totals;
+};
+
+struct vw_stream {
+  vw_ctx* ctx = nullptr;
+  std::vector<double> lo, hi;
+  int L = 0;
+  int boundary = 0;
+  int levels = 0;
+  int64_t last_batch = -1;
+  bool hist_init = false;
+  std::vector<double*> hist;        // device [B][hist_len_j]
+  std::vector<int> hist_len;
+};
+
+static hipEvent_t pool_event(vw_ctx* c) {
+  if (!c->event_pool.empty()) {
+    hipEvent_t e = c->event_pool.back();
+    c->event_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+
+// Brackets a kernel launch with HIP events on the context stream when timing is enabled.
+struct LaunchTimer {
+  vw_ctx* c;
+  TimedLaunch tl;
+  bool on;
+  LaunchTimer(vw_ctx* ctx, const char* family) : c(ctx), on(ctx->timing) {
+    if (!on) return;
+    tl.family = family;
+    tl.start = pool_event(c);
+    tl.stop = pool_event(c);
+    if (!tl.start || !tl.stop) { on = false; return; }
+    hipEventRecord(tl.start, c->stream);
+  }
+  ~LaunchTimer() {
+    if (!on) return;
+    hipEventRecord(tl.stop, c->stream);
+    c->pending.push_back(tl);
+  }
+};
+
+static void collect_timing(vw_ctx* c) {
+  for (auto& tl : c->pending) {
+    float ms = 0.f;
+    if (hipEventSynchronize(tl.stop) == hipSuccess && hipEventElapsedTime(&ms, tl.start, tl.stop) == hipSuccess) {
+      auto& t = c->totals[tl.family];
+      t.first += ms;
+      t.second += 1;
+    }
+    c->event_pool.push_back(tl.start);
+    c->event_pool.push_back(tl.stop);
+  }
+  c->pending.clear();
+}
+
+static vw_status ensure_ws(vw_ctx* c, size_t bytes) {
+  if (bytes <= c->ws_bytes) return VW_OK;
+  if (c->ws) {
+    hipStreamSynchronize(c->stream);
+    hipFree(c->ws);
+    c->ws = nullptr;
+    c->ws_bytes = 0;
+  }
+  size_t want = std::max(bytes, (size_t)1 << 20);
+  VW_HIP(hipMalloc(&c->ws, want));
+  c->ws_bytes = want;
+  return VW_OK;
+}
+
+static inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+static inline int64_t round_up(int64_t v, int64_t a) { return (v + a - 1) / a * a; }
+
+// ------------------------------------------------------------------------------------------------
+// Bookkeeping restated from the reference.
+
+// MultiLevelMODWTTransform.calculateMaxLevels  core/modwt/MultiLevelMODWTTransform.java:455-501
+extern "C" int vw_max_levels(int64_t N, int L) {
+  if (L <= 0 || N <= L) return 0;
+  int max_level = 1;
+  const long long lm1 = L - 1;
+  while (max_level < 10) {
+    const long long scaled = lm1 * (1LL << (max_level - 1)) + 1LL;
+    if (scaled > N) break;
+    max_level++;
+  }
+  return max_level - 1;
+}
+
+extern "C" int64_t vw_upsampled_length(int L, int level) {
+  const int64_t up = (level <= 1) ? 1 : ((int64_t)1 << (level - 1));
+  return (int64_t)(L - 1) * up + 1;
+}
+
+// SymmetricAlignmentStrategy.decide  core/modwt/SymmetricAlignmentStrategy.java:43-117
+static void sym_decide(int wid, int L, int level, int* ap, int* dh, int* dp, int* dg) {
+  int detailPlus = 1, deltaG = 0, deltaH = 0;
+  const bool isHaar = L <= 2;
+  int approxPlus = isHaar ? 1 : 0;
+  if (isHaar) {
+    deltaG = 0;
+    deltaH = (level <= 1) ? 0 : -1;
+  } else if (wid == VW_WID_DB6) {
+    deltaH = (level <= 1) ? 0 : -1;
+    deltaG = (level >= 3) ? 1 : 0;
+  } else if (wid == VW_WID_DB8) {
+    deltaH = (level <= 1) ? 0 : 1;
+    deltaG = (level >= 2) ? 1 : 0;
+  } else if (wid == VW_WID_SYM4) {
+    approxPlus = 1; detailPlus = 0; deltaH = 0; deltaG = 0;
+  } else if (wid == VW_WID_SYM8) {
+    if (level <= 1) { deltaH = 0; deltaG = 0; }
+    else if (level == 2) { deltaH = 1; deltaG = 0; }
+    else { deltaH = 1; deltaG = 1; }
+  } else if (wid == VW_WID_COIF2) {
+    approxPlus = 1; deltaH = (level <= 1) ? 0 : 1; detailPlus = 0; deltaG = 0;
+  } else if (wid == VW_WID_COIF3) {
+    detailPlus = 0;
+    if (level <= 1) { deltaH = 0; deltaG = 0; } else { deltaH = -1; deltaG = 1; }
+  } else if (L >= 12) {
+    if (level <= 1) { deltaH = 0; deltaG = 0; }
+    else { const bool even = level % 2 == 0; deltaH = even ? 0 : -1; deltaG = even ? 0 : -1; }
+  } else {
+    if (level <= 1) { deltaH = 0; deltaG = 0; } else { deltaH = -1; deltaG = 0; }
+  }
+  *ap = approxPlus; *dh = deltaH; *dp = detailPlus; *dg = deltaG;
+}
+
+// MultiLevelMODWTTransform.computeTauJ  core/modwt/MultiLevelMODWTTransform.java:795-806
+static int compute_tau(int base_len, int level) {
+  const int lm1 = base_len - 1;
+  if (level <= 1) return std::max(0, lm1 / 2);
+  const long long up = 1LL << (level - 1);
+  const long long Lj = (long long)lm1 * up + 1LL;
+  const long long tau = (Lj - 1LL) / 2LL;
+  if (tau < 0) return 0;
+  if (tau > 2147483647LL) return 2147483647;
+  return (int)tau;
+}
+
+static int next_pow2(int64_t n) {
+  int64_t p = 1;
+  while (p < n) p <<= 1;
+  return (int)p;
+}
+
+static bool is_pow2(int64_t n) { return n > 0 && (n & (n - 1)) == 0; }
+
+// Level-j input index range read by a branch (dir, off) for outputs t in [0, tmax].
+static void branch_extent(int N, int tmax, int L, int s, int dir, int off, int* hl, int* hr) {
+  const long long reach = (long long)(L - 1) * s;
+  long long mn, mx;
+  if (dir > 0) { mn = off; mx = (long long)tmax + reach + off; }
+  else { mn = (long long)off - reach; mx = (long long)tmax + off; }
+  *hl = (int)std::max<long long>(*hl, -mn);
+  *hr = (int)std::max<long long>(*hr, mx - (N - 1));
+}
+
+template <typename T> static constexpr int vec_width() { return 16 / (int)sizeof(T); }
+
+static bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
+
+// ------------------------------------------------------------------------------------------------
+// Context
+extern "C" vw_status vw_ctx_create(int device, vw_ctx** out) {
+  if (!out) return fail(VW_ERR_NULL, "out is null");
+  int n = 0;
+  VW_HIP(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(VW_ERR_ARG, "device %d out of range (%d devices)", device, n);
+  VW_HIP(hipSetDevice(device));
+  vw_ctx* c = new vw_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(VW_ERR_DEVICE, "hipStreamCreate failed");
+  }
+  c->own_stream = true;
+  if (hipMalloc(&c->bad, sizeof(unsigned long long)) != hipSuccess) {
+    hipStreamDestroy(c->stream);
+    delete c;
+    return fail(VW_ERR_DEVICE, "hipMalloc failed");
+  }
+  *out = c;
+  return ok();
+}
+
+extern "C" vw_status vw_ctx_destroy(vw_ctx* c) {
+  if (!c) return fail(VW_ERR_NULL, "ctx is null");
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  collect_timing(c);
+  for (auto e : c->event_pool) hipEventDestroy(e);
+  if (c->ws) hipFree(c->ws);
+  if (c->ws2) hipFree(c->ws2);
+  if (c->bad) hipFree(c->bad);
+  if (c->own_stream) hipStreamDestroy(c->stream);
+  delete c;
+  return ok();
+}
+
+extern "C" vw_status vw_ctx_set_stream(vw_ctx* c, void* s) {
+  if (!c) return fail(VW_ERR_NULL, "ctx is null");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (c->own_stream) {
+    hipStreamSynchronize(c->stream);
+    hipStreamDestroy(c->stream);
+    c->own_stream = false;
+    c->stream = nullptr;
+  }
+  if (s) {
+    c->stream = (hipStream_t)s;
+  } else {
+    VW_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    c->own_stream = true;
+  }
+  return ok();
+}
+
+extern "C" void* vw_ctx_get_stream(vw_ctx* c) { return c ? (void*)c->stream : nullptr; }
+extern "C" int vw_ctx_device(vw_ctx* c) { return c ? c->device : -1; }
+
+extern "C" vw_status vw_ctx_synchronize(vw_ctx* c) {
+  if (!c) return fail(VW_ERR_NULL, "ctx is null");
+  hipSetDevice(c->device);
+  VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}
+
+extern "C" const char* vw_last_error(void) { return t_err.c_str(); }
+extern "C" int64_t vw_last_error_index(void) { return t_err_index; }
+extern "C" const char* vw_version(void) { return "vectorwave_amd 0.1.0 (gfx950)"; }
+
+extern "C" vw_status vw_ctx_enable_timing(vw_ctx* c, int enable) {
+  if (!c) return fail(VW_ERR_NULL, "ctx is null");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  c->timing = enable != 0;
+  return ok();
+}
+
+extern "C" vw_status vw_ctx_reset_timing(vw_ctx* c) {
+  if (!c) return fail(VW_ERR_NULL, "ctx is null");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  collect_timing(c);
+  c->totals.clear();
+  return ok();
+}
+
+extern "C" vw_status vw_ctx_kernel_time(vw_ctx* c, const char* family, double* total_ms, int64_t* launches) {
+  if (!c || !family) return fail(VW_ERR_NULL, "null argument");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  collect_timing(c);
+  auto it = c->totals.find(family);
+  if (total_ms) *total_ms = it == c->totals.end() ? 0.0 : it->second.first;
+  if (launches) *launches = it == c->totals.end() ? 0 : it->second.second;
+  return ok();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Common argument checks (MultiLevelMODWTTransform.decompose :209-239, BatchMODWT.validateAoS :201-212)
+static vw_status check_common(vw_ctx* c, const void* a, const void* b, const double* lo, const double* hi,
+                              int64_t B, int64_t N, int L, int boundary) {
+  if (!c) return fail(VW_ERR_NULL, "ctx is null");
+  if (!a || !b || !lo || !hi) return fail(VW_ERR_NULL, "null array argument");
+  if (B <= 0) return fail(VW_ERR_EMPTY, "batch must be non-empty (B=%lld)", (long long)B);
+  if (N <= 0) return fail(VW_ERR_EMPTY, "Signal cannot be empty");
+  if (N > (1LL << 30)) return fail(VW_ERR_ARG, "signal length %lld too large", (long long)N);
+  if (boundary < VW_PERIODIC || boundary > VW_ZERO_PADDING)
+    return fail(VW_ERR_BOUNDARY, "MODWT only supports PERIODIC, ZERO_PADDING, and SYMMETRIC boundary modes");
+  if (L < 1 || L > kMaxTaps) return fail(VW_ERR_ARG, "filter length %d unsupported (1..%d)", L, kMaxTaps);
+  return VW_OK;
+}
+
+static vw_status check_levels(int64_t N, int L, int J, unsigned flags) {
+  if (flags & VW_FLAG_CORE_LEVELS) {
+    const int maxl = vw_max_levels(N, L);
+    if (J < 1 || J > maxl)
+      return fail(VW_ERR_LEVEL, "Invalid number of decomposition levels: %d (valid 1..%d for N=%lld, L=%d)", J, maxl,
+                  (long long)N, L);
+  } else {
+    if (J < 1) return fail(VW_ERR_LEVEL, "levels must be >= 1");
+    if (J > kMaxLevels) return fail(VW_ERR_LEVEL, "levels %d exceeds engine limit %d", J, kMaxLevels);
+    if (vw_upsampled_length(L, J) > (int64_t)1 << 30) return fail(VW_ERR_TOO_LARGE, "upsampled filter too long");
+  }
+  return VW_OK;
+}
+
+template <typename T>
+static void copy_taps(T* dst, const double* src, int L) {
+  // base taps * (1.0 / Math.sqrt(2.0)) in double, then rounded to T  (ScalarOps.java:911-914)
+  const double s = 1.0 / std::sqrt(2.0);
+  for (int i = 0; i < L; ++i) dst[i] = (T)(src[i] * s);
+  for (int i = L; i < kMaxTaps; ++i) dst[i] = T(0);
+}
+
+static vw_status read_bad(vw_ctx* c, unsigned long long* out) {
+  VW_HIP(hipMemcpyAsync(out, c->bad, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+  VW_HIP(hipStreamSynchronize(c->stream));
+  return VW_OK;
+}
+
+static vw_status report_bad(unsigned long long bad, int64_t N) {
+  if (bad == ~0ull) return VW_OK;
+  const bool out = (bad >> 62) & 1ull;
+  const unsigned long long flat = bad & ((1ull << 62) - 1);
+  t_err_index = (int64_t)(flat % (unsigned long long)N);
+  return fail(VW_ERR_NONFINITE, "%s contains non-finite value at index %lld (signal %lld)",
+              out ? "coefficients" : "signal", (long long)(flat % (unsigned long long)N),
+              (long long)(flat / (unsigned long long)N));
+}
+
+// Plan of a fused launch: threads, LDS bytes.
+static bool fused_plan(int64_t N, int V, int elem, int64_t lds_elems_extra, int* threads, int* lds) {
+  const int64_t nvec = (N + V - 1) / V;
+  int64_t th = round_up((nvec + kNV - 1) / kNV, 64);
+  th = std::max<int64_t>(th, 64);
+  if (const char* e = getenv("VW_MIN_THREADS")) th = std::max<int64_t>(th, atoi(e));
+  if (th > kMaxThreads) return false;
+  const int64_t bytes = lds_elems_extra * elem;
+  if (bytes > kLdsBytes) return false;
+  *threads = (int)th;
+  *lds = (int)bytes;
+  return true;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Forward (multi-level and single-level share this path).
+template <typename T>
+static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64_t ldx, const double* lo,
+                              const double* hi, int L, int boundary, int J, unsigned flags, T* details, T* approx,
+                              bool single_level, int mode_override, T* const* hist, bool hist_update) {
+  constexpr int V = vec_width<T>();
+  const bool fma = flags & VW_FLAG_FMA;
+  const bool validate = flags & VW_FLAG_VALIDATE;
+  const int64_t nvec = (N + V - 1) / V;
+  const int tmax = (int)(nvec * V - 1);
+  (void)tmax;
+
+  std::vector<LevelDesc> lv(J);
+  int max_hl = 0;
+  const int npow2 = next_pow2(N);
+  for (int j = 1; j <= J; ++j) {
+    LevelDesc& d = lv[j - 1];
+    memset(&d, 0, sizeof(d));
+    d.s = 1 << (j - 1);
+    const int64_t Lj = vw_upsampled_length(L, j);
+    d.hl = (int)(Lj - 1);
+    d.hr = 0;
+    d.hist_len = (int)(Lj - 1);
+    if (boundary == VW_PERIODIC) {
+      d.mode = kHaloPeriodic;
+      // MultiLevelMODWTTransform.applyScaledMODWT :734-742 + FftHeuristics :30-34
+      if ((flags & VW_FLAG_FFT_SWITCH) && !single_level && !(N < 64 || Lj > N / 2) && N >= 1024 &&
+          (double)Lj > N * (1.0 / 8.0) && !is_pow2(N))
+        d.mode = kHaloFftPad;
+    } else {
+      d.mode = boundary == VW_ZERO_PADDING ? kHaloZero : kHaloSymmetric;
+    }
+    if (mode_override >= 0) d.mode = mode_override;
+    max_hl = std::max(max_hl, d.hl);
+  }
+
+  const int hlpad = (int)round_up(max_hl, V);
+  int threads = 0, lds = 0;
+  const int64_t lds_elems = hlpad + nvec * V + V;
+  if (J <= kMaxLevels && fused_plan(N, V, sizeof(T), lds_elems, &threads, &lds) && !getenv("VW_FORCE_TILED")) {
+    FwdArgs<T> a;
+    memset(&a, 0, sizeof(a));
+    a.x = x; a.ldx = ldx; a.details = details; a.approx = approx; a.B = B; a.N = (int)N; a.J = J;
+    a.npow2 = npow2; a.hlpad = hlpad;
+    a.vec_io = (ldx % V == 0) && (N % V == 0) && aligned16(x) && aligned16(details) && aligned16(approx);
+    a.validate = validate; a.bad = c->bad;
+    for (int j = 0; j < J; ++j) a.hist[j] = hist ? hist[j] : nullptr;
+    a.hist_update = hist_update ? 1 : 0;
+    a.taps = L;
+    copy_taps(a.lo, lo, L);
+    copy_taps(a.hi, hi, L);
+    for (int j = 0; j < J; ++j) a.lv[j] = lv[j];
+    if (validate) VW_HIP(hipMemsetAsync(c->bad, 0xFF, sizeof(unsigned long long), c->stream));
+    {
+      LaunchTimer lt(c, "forward");
+      hipError_t e = launch_forward_fused<T>(a, threads, lds, fma, c->stream);
+      if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward launch failed: %s", hipGetErrorString(e));
+    }
+  } else {
+    // Tiled per-level path: ping-pong the running approximation through the workspace.
+    if (hist) return fail(VW_ERR_UNSUPPORTED, "streaming blocks longer than the fused kernel holds in LDS");
+    const int tile_max = 256 * kNV * V;
+    const size_t plane = (size_t)B * (size_t)N;
+    const vw_status st = ensure_ws(c, 2 * plane * sizeof(T) + 256);
+    if (st != VW_OK) return st;
+    T* tmp[2] = {reinterpret_cast<T*>(c->ws), reinterpret_cast<T*>(c->ws) + plane};
+    if (validate) VW_HIP(hipMemsetAsync(c->bad, 0xFF, sizeof(unsigned long long), c->stream));
+    const T* src = x;
+    int64_t lda = ldx;
+    for (int j = 1; j <= J; ++j) {
+      LevelArgs<T> a;
+      memset(&a, 0, sizeof(a));
+      a.lv = lv[j - 1];
+      const int hp = (int)round_up(a.lv.hl, V);
+      // deep levels have long halos: shrink the tile so tile + halo fits LDS
+      const int64_t fit = ((int64_t)kLdsBytes / (int64_t)sizeof(T) - hp - 2 * V) / V * V;
+      const int tile = (int)std::min<int64_t>(tile_max, fit);
+      if (tile < 64 * V) return fail(VW_ERR_UNSUPPORTED, "level %d halo (%d samples) exceeds LDS", j, a.lv.hl);
+      const int64_t elems = hp + tile + V;
+      a.src_a = src; a.lda = lda;
+      a.out_a = (j == J) ? approx : tmp[j & 1];
+      a.out_d = details + (size_t)(j - 1) * plane;
+      a.hist = hist ? hist[j - 1] : nullptr;
+      a.B = B; a.N = (int)N; a.tile = tile; a.hlpad = hp;
+      a.vec_io = (N % V == 0) && aligned16(a.out_a) && aligned16(a.out_d);
+      a.validate = validate; a.bad = c->bad; a.npow2 = npow2; a.taps = L;
+      copy_taps(a.lo, lo, L);
+      copy_taps(a.hi, hi, L);
+      {
+        LaunchTimer lt(c, "forward_level");
+        hipError_t e = launch_forward_level<T>(a, (int)(elems * sizeof(T)), fma, c->stream);
+        if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward level launch failed: %s", hipGetErrorString(e));
+      }
+      src = a.out_a;
+      lda = N;
+    }
+  }
+  if (validate) {
+    unsigned long long bad = 0;
+    vw_status st = read_bad(c, &bad);
+    if (st != VW_OK) return st;
+    st = report_bad(bad, N);
+    if (st != VW_OK) return st;
+  }
+  if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  return VW_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Inverse
+template <typename T>
+static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int64_t B, int64_t N, const double* lo,
+                              const double* hi, int L, int wid, int boundary, int J, unsigned detail_mask,
+                              int approx_zero, unsigned flags, T* y, bool single_level, const T* thr, int soft) {
+  constexpr int V = vec_width<T>();
+  const bool fma = flags & VW_FLAG_FMA;
+  const int64_t nvec = (N + V - 1) / V;
+  const int tmax = (int)(nvec * V - 1);
+  const bool pair = single_level || boundary == VW_ZERO_PADDING;
+
+  std::vector<LevelDesc> lv(J);
+  int max_hl = 0, max_hr = 0;
+  for (int j = 1; j <= J; ++j) {
+    LevelDesc& d = lv[j - 1];
+    memset(&d, 0, sizeof(d));
+    d.s = 1 << (j - 1);
+    d.use_d = (detail_mask >> (j - 1)) & 1u;
+    d.mode = boundary == VW_PERIODIC ? kHaloPeriodic : boundary == VW_ZERO_PADDING ? kHaloZero : kHaloSymmetric;
+    if (boundary == VW_SYMMETRIC && !single_level) {
+      int ap, dh, dp, dg;
+      sym_decide(wid, L, j, &ap, &dh, &dp, &dg);
+      const int tauH = compute_tau(L, j) + dh;
+      const int tauG = compute_tau(L, j) + dg;
+      d.dir_a = ap ? 1 : -1; d.off_a = ap ? -tauH : tauH;
+      d.dir_d = dp ? 1 : -1; d.off_d = dp ? -tauG : tauG;
+    } else if (boundary == VW_SYMMETRIC) {
+      const int dir = (flags & VW_FLAG_BATCH_SYM_INVERSE) ? 1 : -1;  // inverseBatchOptimized (t+l) vs inverse (t-l)
+      d.dir_a = d.dir_d = dir; d.off_a = d.off_d = 0;
+    } else {
+      d.dir_a = d.dir_d = 1; d.off_a = d.off_d = 0;
+    }
+    int hl = 0, hr = 0;
+    branch_extent((int)N, tmax, L, d.s, d.dir_a, d.off_a, &hl, &hr);
+    branch_extent((int)N, tmax, L, d.s, d.dir_d, d.off_d, &hl, &hr);
+    d.hl = hl; d.hr = hr;
+    max_hl = std::max(max_hl, hl);
+    max_hr = std::max(max_hr, hr);
+  }
+  const int hlpad = (int)round_up(max_hl, V);
+  const int64_t region = round_up(hlpad + nvec * V + max_hr + V, V);
+  int threads = 0, lds = 0;
+  if (fused_plan(N, V, sizeof(T), 2 * region, &threads, &lds) && !getenv("VW_FORCE_TILED")) {
+    InvArgs<T> a;
+    memset(&a, 0, sizeof(a));
+    a.details = details; a.approx = approx; a.y = y; a.B = B; a.N = (int)N; a.J = J;
+    a.hlpad_a = hlpad; a.hlpad_d = hlpad; a.region_d = (int)region;
+    a.vec_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
+    a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.soft = soft; a.taps = L;
+    copy_taps(a.lo, lo, L);
+    copy_taps(a.hi, hi, L);
+    for (int j = 0; j < J; ++j) a.lv[j] = lv[j];
+    LaunchTimer lt(c, "inverse");
+    hipError_t e = launch_inverse_fused<T>(a, threads, lds, fma, c->stream);
+    if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse launch failed: %s", hipGetErrorString(e));
+  } else {
+    const int tile_max = 256 * kNV * V;
+    const size_t plane = (size_t)B * (size_t)N;
+    const vw_status st = ensure_ws(c, 2 * plane * sizeof(T) + 256);
+    if (st != VW_OK) return st;
+    T* tmp[2] = {reinterpret_cast<T*>(c->ws), reinterpret_cast<T*>(c->ws) + plane};
+    const T* cur = approx_zero ? nullptr : approx;
+    for (int j = J; j >= 1; --j) {
+      LevelArgs<T> a;
+      memset(&a, 0, sizeof(a));
+      a.lv = lv[j - 1];
+      const int hp = (int)round_up(a.lv.hl, V);
+      const int64_t fit = ((int64_t)kLdsBytes / (int64_t)sizeof(T) / 2 - hp - a.lv.hr - 2 * V) / V * V;
+      const int tile = (int)std::min<int64_t>(tile_max, fit);
+      if (tile < 64 * V) return fail(VW_ERR_UNSUPPORTED, "level %d halo exceeds LDS", j);
+      const int64_t reg = round_up(hp + tile + a.lv.hr + V, V);
+      a.src_a = cur;
+      a.src_d = a.lv.use_d ? details + (size_t)(j - 1) * plane : nullptr;
+      a.use_d = a.lv.use_d;
+      a.out_a = (j == 1) ? y : tmp[j & 1];
+      a.B = B; a.N = (int)N; a.tile = tile; a.hlpad = hp; a.hlpad_d = hp; a.region_d = (int)reg;
+      a.pair = pair; a.thr = thr; a.soft = soft; a.taps = L;
+      a.vec_io = (N % V == 0) && aligned16(a.out_a);
+      copy_taps(a.lo, lo, L);
+      copy_taps(a.hi, hi, L);
+      LaunchTimer lt(c, "inverse_level");
+      hipError_t e = launch_inverse_level<T>(a, (int)(2 * reg * sizeof(T)), fma, c->stream);
+      if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse level launch failed: %s", hipGetErrorString(e));
+      cur = a.out_a;
+    }
+  }
+  if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  return VW_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Host-memory staging (the JNI / FFM path): copy in, run on device, copy out, synchronize.
+struct Staging {
+  vw_ctx* c;
+  std::vector<std::pair<void*, size_t>> allocs;
+  explicit Staging(vw_ctx* ctx) : c(ctx) {}
+  ~Staging() {
+    hipStreamSynchronize(c->stream);
+    for (auto& a : allocs) hipFree(a.first);
+  }
+  template <typename T>
+  vw_status in(const T* host, size_t count, T** dev) {
+    void* p = nullptr;
+    VW_HIP(hipMalloc(&p, std::max<size_t>(count * sizeof(T), 16)));
+    allocs.push_back({p, count});
+    if (host && count) VW_HIP(hipMemcpyAsync(p, host, count * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    *dev = reinterpret_cast<T*>(p);
+    return VW_OK;
+  }
+  template <typename T>
+  vw_status out(T* host, const T* dev, size_t count) {
+    if (host && count) VW_HIP(hipMemcpyAsync(host, dev, count * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+    return VW_OK;
+  }
+};
+
+#define VW_TRY(expr)                      \
+  do {                                    \
+    vw_status s_ = (expr);                \
+    if (s_ != VW_OK) return s_;           \
+  } while (0)
+
+template <typename T>
+static vw_status modwt_forward(vw_ctx* c, const T* x, int64_t B, int64_t N, int64_t ldx, const double* lo,
+                               const double* hi, int L, int wid, int boundary, int J, unsigned flags, T* details,
+                               T* approx) {
+  (void)wid;
+  VW_TRY(check_common(c, x, details, lo, hi, B, N, L, boundary));
+  if (!approx) return fail(VW_ERR_NULL, "approx is null");
+  if (ldx < N) return fail(VW_ERR_ARG, "ldx (%lld) < N (%lld)", (long long)ldx, (long long)N);
+  VW_TRY(check_levels(N, L, J, flags));
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (flags & VW_FLAG_HOST_MEMORY) {
+    Staging s(c);
+    T *dx, *dd, *da;
+    VW_TRY(s.in(x, (size_t)B * ldx, &dx));
+    VW_TRY(s.in<T>(nullptr, (size_t)J * B * N, &dd));
+    VW_TRY(s.in<T>(nullptr, (size_t)B * N, &da));
+    VW_TRY(forward_impl<T>(c, dx, B, N, ldx, lo, hi, L, boundary, J, flags & ~VW_FLAG_SYNC, dd, da, false, -1,
+                           nullptr, false));
+    VW_TRY(s.out(details, dd, (size_t)J * B * N));
+    VW_TRY(s.out(approx, da, (size_t)B * N));
+    VW_HIP(hipStreamSynchronize(c->stream));
+    return ok();
+  }
+  VW_TRY(forward_impl<T>(c, x, B, N, ldx, lo, hi, L, boundary, J, flags, details, approx, false, -1, nullptr, false));
+  return ok();
+}
+
+template <typename T>
+static vw_status modwt_inverse(vw_ctx* c, const T* details, const T* approx, int64_t B, int64_t N, const double* lo,
+                               const double* hi, int L, int wid, int boundary, int J, unsigned detail_mask,
+                               int approx_zero, unsigned flags, T* y) {
+  if (!c) return fail(VW_ERR_NULL, "ctx is null");
+  if (!y || !lo || !hi) return fail(VW_ERR_NULL, "null argument");
+  if (!details && detail_mask) return fail(VW_ERR_NULL, "details is null");
+  if (!approx && !approx_zero) return fail(VW_ERR_NULL, "approx is null");
+  VW_TRY(check_common(c, y, y, lo, hi, B, N, L, boundary));
+  if (J < 1 || J > kMaxLevels) return fail(VW_ERR_LEVEL, "levels must be in 1..%d", kMaxLevels);
+  // applyScaledInverseMODWT guard :561-574 (reconstruct has no level cap, only L_j <= N); the SWT
+  // periodic inverse (VectorWaveSwtAdapter.reconstructPeriodic :444-474) wraps instead.
+  if ((flags & VW_FLAG_CORE_LEVELS) && vw_upsampled_length(L, J) > N)
+    return fail(VW_ERR_TOO_LARGE, "Upsampled reconstruction filter length exceeds signal length");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (flags & VW_FLAG_HOST_MEMORY) {
+    Staging s(c);
+    T *dd = nullptr, *da = nullptr, *dy;
+    if (detail_mask) VW_TRY(s.in(details, (size_t)J * B * N, &dd));
+    if (!approx_zero) VW_TRY(s.in(approx, (size_t)B * N, &da));
+    VW_TRY(s.in<T>(nullptr, (size_t)B * N, &dy));
+    VW_TRY(inverse_impl<T>(c, dd, da, B, N, lo, hi, L, wid, boundary, J, detail_mask, approx_zero,
+                           flags & ~VW_FLAG_SYNC, dy, false, nullptr, 0));
+    VW_TRY(s.out(y, dy, (size_t)B * N));
+    VW_HIP(hipStreamSynchronize(c->stream));
+    return ok();
+  }
+  VW_TRY(inverse_impl<T>(c, details, approx, B, N, lo, hi, L, wid, boundary, J, detail_mask, approx_zero, flags, y,
+                         false, nullptr, 0));
+  return ok();
+}
+
+extern "C" vw_status vw_modwt_forward_f64(vw_ctx* c, const double* x, int64_t B, int64_t N, int64_t ldx,
+                                          const double* lo, const double* hi, int L, int wid, int boundary, int J,
+                                          unsigned flags, double* details, double* approx) {
+  return modwt_forward<double>(c, x, B, N, ldx, lo, hi, L, wid, boundary, J, flags, details, approx);
+}
+extern "C" vw_status vw_modwt_forward_f32(vw_ctx* c, const float* x, int64_t B, int64_t N, int64_t ldx,
+                                          const double* lo, const double* hi, int L, int wid, int boundary, int J,
+                                          unsigned flags, float* details, float* approx) {
+  return modwt_forward<float>(c, x, B, N, ldx, lo, hi, L, wid, boundary, J, flags, details, approx);
+}
+extern "C" vw_status vw_modwt_inverse_f64(vw_ctx* c, const double* details, const double* approx, int64_t B,
+                                          int64_t N, const double* lo, const double* hi, int L, int wid, int boundary,
+                                          int J, unsigned detail_mask, int approx_zero, unsigned flags, double* y) {
+  return modwt_inverse<double>(c, details, approx, B, N, lo, hi, L, wid, boundary, J, detail_mask, approx_zero,
+                               flags, y);
+}
+extern "C" vw_status vw_modwt_inverse_f32(vw_ctx* c, const float* details, const float* approx, int64_t B,
+                                          int64_t N, const double* lo, const double* hi, int L, int wid, int boundary,
+                                          int J, unsigned detail_mask, int approx_zero, unsigned flags, float* y) {
+  return modwt_inverse<float>(c, details, approx, B, N, lo, hi, L, wid, boundary, J, detail_mask, approx_zero, flags,
+                              y);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Single level (MODWTTransform): any N >= 1 (no L <= N guard), pairwise inverse sums.
+extern "C" vw_status vw_modwt1_forward_f64(vw_ctx* c, const double* x, int64_t B, int64_t N, int64_t ldx,
+                                           const double* lo, const double* hi, int L, int boundary, unsigned flags,
+                                           double* approx, double* detail) {
+  VW_TRY(check_common(c, x, detail, lo, hi, B, N, L, boundary));
+  if (!approx) return fail(VW_ERR_NULL, "approx is null");
+  if (ldx < N) return fail(VW_ERR_ARG, "ldx < N");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  const bool haar_quirk = (flags & VW_FLAG_BATCH_HAAR) && L == 2 && boundary == VW_PERIODIC;
+  auto run = [&](const double* dx, double* da, double* dd, unsigned fl) -> vw_status {
+    if (haar_quirk) {
+      LaunchTimer lt(c, "forward1");
+      hipError_t e = launch_single_haar_batch<double>(dx, ldx, B, (int)N, da, dd, c->stream);
+      if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+      return VW_OK;
+    }
+    return forward_impl<double>(c, dx, B, N, ldx, lo, hi, L, boundary, 1, fl & ~VW_FLAG_FFT_SWITCH, dd, da, true,
+                                -1, nullptr, false);
+  };
+  if (flags & VW_FLAG_HOST_MEMORY) {
+    Staging s(c);
+    double *dx, *da, *dd;
+    VW_TRY(s.in(x, (size_t)B * ldx, &dx));
+    VW_TRY(s.in<double>(nullptr, (size_t)B * N, &da));
+    VW_TRY(s.in<double>(nullptr, (size_t)B * N, &dd));
+    VW_TRY(run(dx, da, dd, flags & ~VW_FLAG_SYNC));
+    VW_TRY(s.out(approx, da, (size_t)B * N));
+    VW_TRY(s.out(detail, dd, (size_t)B * N));
+    VW_HIP(hipStreamSynchronize(c->stream));
+    return ok();
+  }
+  VW_TRY(run(x, approx, detail, flags));
+  if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}
+
+extern "C" vw_status vw_modwt1_inverse_f64(vw_ctx* c, const double* approx, const double* detail, int64_t B,
+                                           int64_t N, const double* lo, const double* hi, int L, int boundary,
+                                           unsigned flags, double* y) {
+  VW_TRY(check_common(c, approx, detail, lo, hi, B, N, L, boundary));
+  if (!y) return fail(VW_ERR_NULL, "y is null");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (flags & VW_FLAG_HOST_MEMORY) {
+    Staging s(c);
+    double *da, *dd, *dy;
+    VW_TRY(s.in(approx, (size_t)B * N, &da));
+    VW_TRY(s.in(detail, (size_t)B * N, &dd));
+    VW_TRY(s.in<double>(nullptr, (size_t)B * N, &dy));
+    VW_TRY(inverse_impl<double>(c, dd, da, B, N, lo, hi, L, VW_WID_OTHER, boundary, 1, 1u, 0, flags & ~VW_FLAG_SYNC,
+                                dy, true, nullptr, 0));
+    VW_TRY(s.out(y, dy, (size_t)B * N));
+    VW_HIP(hipStreamSynchronize(c->stream));
+    return ok();
+  }
+  VW_TRY(inverse_impl<double>(c, detail, approx, B, N, lo, hi, L, VW_WID_OTHER, boundary, 1, 1u, 0, flags, y, true,
+                              nullptr, 0));
+  return ok();
+}
+
+// ------------------------------------------------------------------------------------------------
+// SWT denoise: fused forward -> per-signal exact median of |d_1| -> inverse with fused threshold.
+extern "C" vw_status vw_noise_sigma_f64(vw_ctx* c, const double* coeffs, int64_t B, int64_t N, unsigned flags,
+                                        double* sigma) {
+  if (!c || !coeffs || !sigma) return fail(VW_ERR_NULL, "null argument");
+  if (B <= 0 || N <= 0) return fail(VW_ERR_EMPTY, "empty input");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (flags & VW_FLAG_HOST_MEMORY) {
+    Staging s(c);
+    double *dc, *ds;
+    VW_TRY(s.in(coeffs, (size_t)B * N, &dc));
+    VW_TRY(s.in<double>(nullptr, (size_t)B, &ds));
+    hipError_t e = launch_noise_sigma(dc, N, B, (int)N, 0.0, ds, nullptr, c->stream);
+    if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+    VW_TRY(s.out(sigma, ds, (size_t)B));
+    VW_HIP(hipStreamSynchronize(c->stream));
+    return ok();
+  }
+  hipError_t e = launch_noise_sigma(coeffs, N, B, (int)N, 0.0, sigma, nullptr, c->stream);
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+  if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}
+
+extern "C" vw_status vw_threshold_f64(vw_ctx* c, double* coeffs, int64_t B, int64_t N, const double* thr, int soft,
+                                      unsigned flags) {
+  if (!c || !coeffs || !thr) return fail(VW_ERR_NULL, "null argument");
+  if (B <= 0 || N <= 0) return fail(VW_ERR_EMPTY, "empty input");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (flags & VW_FLAG_HOST_MEMORY) {
+    Staging s(c);
+    double *dc, *dt;
+    VW_TRY(s.in(coeffs, (size_t)B * N, &dc));
+    VW_TRY(s.in(thr, (size_t)B, &dt));
+    hipError_t e = launch_threshold<double>(dc, B, N, dt, soft, c->stream);
+    if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+    VW_TRY(s.out(coeffs, dc, (size_t)B * N));
+    VW_HIP(hipStreamSynchronize(c->stream));
+    return ok();
+  }
+  hipError_t e = launch_threshold<double>(coeffs, B, N, thr, soft, c->stream);
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+  if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}
+
+static vw_status denoise_device(vw_ctx* c, const double* x, int64_t B, int64_t N, int64_t ldx, const double* lo,
+                                const double* hi, int L, int wid, int boundary, int J, double threshold, int soft,
+                                unsigned flags, double* y, double* thr_out) {
+  const size_t plane = (size_t)B * (size_t)N;
+  // workspace: details [J][B][N] | approx [B][N] | thr [B]   (tiled levels use ws beyond, via a 2nd alloc)
+  const size_t bytes = align_up(((size_t)J + 1) * plane * sizeof(double), 256) + align_up((size_t)B * 8, 256);
+  if (bytes > c->ws2_bytes) {
+    if (c->ws2) {
+      hipStreamSynchronize(c->stream);
+      hipFree(c->ws2);
+      c->ws2 = nullptr;
+      c->ws2_bytes = 0;
+    }
+    VW_HIP(hipMalloc(&c->ws2, bytes));
+    c->ws2_bytes = bytes;
+  }
+  void* buf = c->ws2;
+  double* det = reinterpret_cast<double*>(buf);
+  double* app = det + (size_t)J * plane;
+  double* thr = reinterpret_cast<double*>(reinterpret_cast<char*>(buf) +
+                                          align_up(((size_t)J + 1) * plane * sizeof(double), 256));
+  vw_status st = forward_impl<double>(c, x, B, N, ldx, lo, hi, L, boundary, J, flags & ~VW_FLAG_SYNC, det, app, false,
+                                      -1, nullptr, false);
+  if (st == VW_OK) {
+    hipError_t e;
+    if (threshold < 0) {
+      // T = sigma * Math.sqrt(2 * Math.log(n))  core/swt/VectorWaveSwtAdapter.java:514
+      const double scale_c = std::sqrt(2 * std::log((double)N));
+      LaunchTimer lt(c, "sigma");
+      e = launch_noise_sigma(det, N, B, (int)N, scale_c, nullptr, thr, c->stream);
+    } else {
+      std::vector<double> h((size_t)B, threshold);
+      e = hipMemcpyAsync(thr, h.data(), (size_t)B * sizeof(double), hipMemcpyHostToDevice, c->stream);
+      if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    }
+    if (e != hipSuccess) st = fail(VW_ERR_DEVICE, "threshold stage failed: %s", hipGetErrorString(e));
+  }
+  if (st == VW_OK)
+    st = inverse_impl<double>(c, det, app, B, N, lo, hi, L, wid, boundary, J, ~0u, 0, flags & ~VW_FLAG_SYNC, y, false,
+                              thr, soft);
+  if (st == VW_OK && thr_out) {
+    hipError_t e = hipMemcpyAsync(thr_out, thr, (size_t)B * sizeof(double), hipMemcpyDeviceToDevice, c->stream);
+    if (e != hipSuccess) st = fail(VW_ERR_DEVICE, "copy failed");
+  }
+  return st;
+}
+
+extern "C" vw_status vw_swt_denoise_f64(vw_ctx* c, const double* x, int64_t B, int64_t N, int64_t ldx,
+                                        const double* lo, const double* hi, int L, int wid, int boundary, int J,
+                                        double threshold, int soft, unsigned flags, double* y,
+                                        double* thresholds_out) {
+  VW_TRY(check_common(c, x, y, lo, hi, B, N, L, boundary));
+  if (ldx < N) return fail(VW_ERR_ARG, "ldx < N");
+  VW_TRY(check_levels(N, L, J, flags));
+  if (vw_upsampled_length(L, J) > N && boundary != VW_PERIODIC)
+    return fail(VW_ERR_TOO_LARGE, "Upsampled reconstruction filter length exceeds signal length");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (flags & VW_FLAG_HOST_MEMORY) {
+    Staging s(c);
+    double *dx, *dy, *dt = nullptr;
+    VW_TRY(s.in(x, (size_t)B * ldx, &dx));
+    VW_TRY(s.in<double>(nullptr, (size_t)B * N, &dy));
+    if (thresholds_out) VW_TRY(s.in<double>(nullptr, (size_t)B, &dt));
+    VW_TRY(denoise_device(c, dx, B, N, ldx, lo, hi, L, wid, boundary, J, threshold, soft, flags, dy, dt));
+    VW_TRY(s.out(y, dy, (size_t)B * N));
+    if (thresholds_out) VW_TRY(s.out(thresholds_out, dt, (size_t)B));
+    VW_HIP(hipStreamSynchronize(c->stream));
+    return ok();
+  }
+  VW_TRY(denoise_device(c, x, B, N, ldx, lo, hi, L, wid, boundary, J, threshold, soft, flags, y, thresholds_out));
+  if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Streaming (BatchStreamingMODWT)
+extern "C" vw_status vw_stream_create(vw_ctx* c, const double* lo, const double* hi, int L, int boundary, int levels,
+                                      vw_stream** out) {
+  if (!c || !lo || !hi || !out) return fail(VW_ERR_NULL, "null argument");
+  if (levels < 1) return fail(VW_ERR_ARG, "levels must be >= 1");
+  if (levels > kMaxLevels) return fail(VW_ERR_ARG, "levels too large");
+  if (L < 1 || L > kMaxTaps) return fail(VW_ERR_ARG, "bad filter length");
+  if (boundary < VW_PERIODIC || boundary > VW_ZERO_PADDING) return fail(VW_ERR_BOUNDARY, "bad boundary");
+  vw_stream* s = new vw_stream();
+  s->ctx = c;
+  s->lo.assign(lo, lo + L);
+  s->hi.assign(hi, hi + L);
+  s->L = L;
+  s->boundary = boundary;
+  s->levels = levels;
+  s->hist.assign(levels, nullptr);
+  s->hist_len.resize(levels);
+  for (int j = 1; j <= levels; ++j) s->hist_len[j - 1] = (int)(vw_upsampled_length(L, j) - 1);
+  *out = s;
+  return ok();
+}
+
+static void free_hist(vw_stream* s) {
+  for (auto& p : s->hist) {
+    if (p) hipFree(p);
+    p = nullptr;
+  }
+}
+
+extern "C" vw_status vw_stream_destroy(vw_stream* s) {
+  if (!s) return fail(VW_ERR_NULL, "stream is null");
+  hipSetDevice(s->ctx->device);
+  hipStreamSynchronize(s->ctx->stream);
+  free_hist(s);
+  delete s;
+  return ok();
+}
+
+extern "C" int64_t vw_stream_history_length(vw_stream* s, int level) {
+  if (!s || level < 1 || level > s->levels) return -1;
+  return s->hist_len[level - 1];
+}
+
+static vw_status stream_run(vw_stream* s, const double* blk, int64_t B, int64_t n, unsigned flags, double* details,
+                            double* approx, bool flush) {
+  vw_ctx* c = s->ctx;
+  if (s->boundary == VW_PERIODIC) {
+    // processMultiLevel PERIODIC -> BatchMODWT.multiLevelAoS (no cap), BatchStreamingMODWT.java:115-116
+    return forward_impl<double>(c, blk, B, n, n, s->lo.data(), s->hi.data(), s->L, s->boundary, s->levels,
+                                flags & ~VW_FLAG_SYNC, details, approx, false, -1, nullptr, false);
+  }
+  const bool first = !s->hist_init;
+  const int mode = first ? -1 : kHaloHistory;
+  return forward_impl<double>(c, blk, B, n, n, s->lo.data(), s->hi.data(), s->L, s->boundary, s->levels,
+                              flags & ~VW_FLAG_SYNC, details, approx, false, mode, s->hist.data(), !flush);
+}
+
+extern "C" vw_status vw_stream_process_f64(vw_stream* s, const double* block, int64_t B, int64_t n, unsigned flags,
+                                           double* details, double* approx) {
+  if (!s) return fail(VW_ERR_NULL, "stream is null");
+  vw_ctx* c = s->ctx;
+  VW_TRY(check_common(c, block, details, s->lo.data(), s->hi.data(), B, n, s->L, s->boundary));
+  if (!approx) return fail(VW_ERR_NULL, "approx is null");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (s->boundary != VW_PERIODIC) {
+    // ensureHistoryCapacity  BatchStreamingMODWT.java:310-324: batch change re-initialises history
+    if (s->last_batch != B) {
+      free_hist(s);
+      for (int j = 0; j < s->levels; ++j)
+        VW_HIP(hipMalloc(&s->hist[j], std::max<size_t>((size_t)B * s->hist_len[j] * sizeof(double), 16)));
+      s->hist_init = false;
+      s->last_batch = B;
+    }
+  }
+  vw_status st;
+  if (flags & VW_FLAG_HOST_MEMORY) {
+    Staging sg(c);
+    double *db, *dd, *da;
+    VW_TRY(sg.in(block, (size_t)B * n, &db));
+    VW_TRY(sg.in<double>(nullptr, (size_t)s->levels * B * n, &dd));
+    VW_TRY(sg.in<double>(nullptr, (size_t)B * n, &da));
+    st = stream_run(s, db, B, n, flags, dd, da, false);
+    if (st != VW_OK) return st;
+    VW_TRY(sg.out(details, dd, (size_t)s->levels * B * n));
+    VW_TRY(sg.out(approx, da, (size_t)B * n));
+    VW_HIP(hipStreamSynchronize(c->stream));
+  } else {
+    st = stream_run(s, block, B, n, flags, details, approx, false);
+    if (st != VW_OK) return st;
+    if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  }
+  if (s->boundary != VW_PERIODIC) s->hist_init = true;
+  return ok();
+}
+
+// flushMultiLevel  BatchStreamingMODWT.java:231-275: tail from level-1 history (ZERO: zeros;
+// SYMMETRIC: hist[histLen-1-t]), run through every level's history without updating it.
+extern "C" vw_status vw_stream_flush_f64(vw_stream* s, int64_t tail_len, unsigned flags, double* details,
+                                         double* approx) {
+  if (!s) return fail(VW_ERR_NULL, "stream is null");
+  vw_ctx* c = s->ctx;
+  if (s->boundary == VW_PERIODIC) return fail(VW_ERR_UNSUPPORTED, "Flush is only applicable to ZERO_PADDING/SYMMETRIC");
+  if (tail_len <= 0) return ok();
+  if (!s->hist_init || s->last_batch <= 0) return fail(VW_ERR_STATE, "No prior blocks processed; cannot flush");
+  int min_hist = s->hist_len[0];
+  for (int j = 0; j < s->levels; ++j) min_hist = std::min(min_hist, s->hist_len[j]);
+  if (tail_len > min_hist)
+    return fail(VW_ERR_ARG, "tailLength (%lld) exceeds maximum allowed across levels (%d)", (long long)tail_len,
+                min_hist);
+  if (!details || !approx) return fail(VW_ERR_NULL, "null output");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  const int64_t B = s->last_batch;
+  const int h0 = s->hist_len[0];
+  std::vector<double> hist((size_t)B * h0), tail((size_t)B * tail_len, 0.0);
+  if (s->boundary == VW_SYMMETRIC) {
+    VW_HIP(hipMemcpyAsync(hist.data(), s->hist[0], hist.size() * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    VW_HIP(hipStreamSynchronize(c->stream));
+    for (int64_t b = 0; b < B; ++b)
+      for (int64_t t = 0; t < tail_len; ++t) tail[b * tail_len + t] = hist[b * h0 + (h0 - 1 - t)];
+  }
+  Staging sg(c);
+  double *dt, *dd = nullptr, *da = nullptr;
+  VW_TRY(sg.in(tail.data(), tail.size(), &dt));
+  const bool host = flags & VW_FLAG_HOST_MEMORY;
+  if (host) {
+    VW_TRY(sg.in<double>(nullptr, (size_t)s->levels * B * tail_len, &dd));
+    VW_TRY(sg.in<double>(nullptr, (size_t)B * tail_len, &da));
+  }
+  VW_TRY(forward_impl<double>(c, dt, B, tail_len, tail_len, s->lo.data(), s->hi.data(), s->L, s->boundary, s->levels,
+                              flags & ~VW_FLAG_SYNC, host ? dd : details, host ? da : approx, false, kHaloHistory,
+                              s->hist.data(), false));
+  if (host) {
+    VW_TRY(sg.out(details, dd, (size_t)s->levels * B * tail_len));
+    VW_TRY(sg.out(approx, da, (size_t)B * tail_len));
+  }
+  VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Device utilities
+extern "C" vw_status vw_fill_uniform_f64(vw_ctx* c, double* x, int64_t count, uint64_t seed, int64_t offset) {
+  if (!c || !x) return fail(VW_ERR_NULL, "null argument");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  hipError_t e = launch_fill_uniform<double>(x, count, seed, offset, c->stream);
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+  return ok();
+}
+
+extern "C" vw_status vw_fill_uniform_f32(vw_ctx* c, float* x, int64_t count, uint64_t seed, int64_t offset) {
+  if (!c || !x) return fail(VW_ERR_NULL, "null argument");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  hipError_t e = launch_fill_uniform<float>(x, count, seed, offset, c->stream);
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+  return ok();
+}
+
+extern "C" vw_status vw_device_alloc(vw_ctx* c, int64_t bytes, void** out) {
+  if (!c || !out) return fail(VW_ERR_NULL, "null argument");
+  hipSetDevice(c->device);
+  VW_HIP(hipMalloc(out, (size_t)std::max<int64_t>(bytes, 16)));
+  return ok();
+}
+
+extern "C" vw_status vw_device_free(vw_ctx* c, void* p) {
+  if (!c) return fail(VW_ERR_NULL, "null argument");
+  hipSetDevice(c->device);
+  if (p) VW_HIP(hipFree(p));
+  return ok();
+}
+
+extern "C" vw_status vw_memcpy(vw_ctx* c, void* dst, const void* src, int64_t bytes, int kind) {
+  if (!c || !dst || !src) return fail(VW_ERR_NULL, "null argument");
+  hipSetDevice(c->device);
+  const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost
+                                                                        : hipMemcpyDeviceToDevice;
+  VW_HIP(hipMemcpyAsync(dst, src, (size_t)bytes, k, c->stream));
+  VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}

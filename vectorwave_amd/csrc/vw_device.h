@@ -1,0 +1,766 @@
+#pragma once
+// vw_device.h -- hand-written CDNA4 (gfx950) HIP kernels for VectorWave's MODWT / SWT hot path.
+//
+// The hot loop of the reference is the a-trous convolution of one level:
+//   forward  (K1-K3)  out[t] = sum_{l=0}^{L_j-1} f_j[l] * x[g(t - l)]           ScalarOps.java:700-835
+//   inverse  (K4-K6)  y[t]   = sum_l h_j[l] * a[g(t +/- l - tau)] (+) sum_l g_j[l] * d[...]
+//                                                                  MultiLevelMODWTTransform.java:554-645
+// with f_j the base taps * 1/sqrt(2) upsampled by 2^(j-1) (ScalarOps.java:909-916).  Only the L
+// non-zero taps at spacing s = 2^(j-1) contribute; the zero taps add +/-0.0 to a sum that is never
+// -0.0, so skipping them is exact.
+//
+// MI355X design:
+//  * One workgroup per signal.  The whole level input lives in LDS with its boundary "halo"
+//    materialised around it, so the inner loop is boundary-agnostic: the reference's index map g
+//    (periodic wrap, zero padding, half-sample mirror, FFT zero-pad, streaming history) is applied
+//    once per level when the halo is filled, not once per tap.
+//  * The J-level cascade is fused: x is read from HBM once, each detail level is written once,
+//    the running approximation never leaves LDS / VGPRs (forward); the inverse reads each detail
+//    level once (prefetched into VGPRs while the previous level computes) and writes y once.
+//  * Each lane owns 16-byte vectors of consecutive outputs (2 x fp64 / 4 x fp32): global loads
+//    and stores are dwordx4 and fully coalesced; LDS reads are ds_read_b128 at spacing s, or one
+//    register window for s < vector width (level 1), conflict-free (consecutive lanes, consecutive
+//    16-byte slots).
+//  * EXACT variant: separate v_mul_f64 / v_add_f64 in the reference's tap order (file compiled with
+//    -ffp-contract=off): bit-identical to vectorwave-core.  FMA variant: v_fma_f64, ~1 ulp/tap.
+//  * Bandwidth-bound stencil: no MFMA.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "vw_internal.h"
+
+#pragma clang fp contract(off)
+
+namespace vw {
+
+template <typename T> struct VT;
+template <> struct VT<double> { typedef double v __attribute__((ext_vector_type(2))); static constexpr int V = 2; };
+template <> struct VT<float>  { typedef float  v __attribute__((ext_vector_type(4))); static constexpr int V = 4; };
+
+__device__ __forceinline__ double fma_t(double a, double b, double c) { return __builtin_fma(a, b, c); }
+__device__ __forceinline__ float fma_t(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
+
+// acc + x*f : EXACT = rounded product then rounded sum (Java semantics); FMA = one rounding.
+template <bool FMA, typename T>
+__device__ __forceinline__ T madd(T acc, T x, T f) {
+  if constexpr (FMA) return fma_t(x, f, acc);
+  else return acc + x * f;
+}
+
+__device__ __forceinline__ bool finite_t(double v) { return __builtin_isfinite(v); }
+__device__ __forceinline__ bool finite_t(float v) { return __builtin_isfinite(v); }
+
+// MathUtils.symmetricBoundaryExtension  core/util/MathUtils.java:30-51
+__device__ __forceinline__ int sym_index(int idx, int n) {
+  if (idx >= 0 && idx < n) return idx;
+  int period = 2 * n;
+  idx = ((idx % period) + period) % period;
+  if (idx >= n) idx = period - idx - 1;
+  return idx;
+}
+
+// Value of a level input at signal index idx outside [0, N), read from the LDS copy `buf`
+// (element 0 at buf[0]).  The reference's index maps; see HaloMode.
+template <typename T>
+__device__ __forceinline__ T halo_value_lds(const T* buf, int idx, int N, int mode, int npow2,
+                                            const T* hist_b, int hist_len) {
+  switch (mode) {
+    case kHaloPeriodic: { int r = idx % N; if (r < 0) r += N; return buf[r]; }
+    case kHaloSymmetric: return buf[sym_index(idx, N)];
+    case kHaloFftPad: { int r = idx < 0 ? idx + npow2 : idx; return (r >= 0 && r < N) ? buf[r] : T(0); }
+    case kHaloHistory: return (idx < 0 && idx >= -hist_len) ? hist_b[hist_len + idx] : T(0);
+    default: return T(0);
+  }
+}
+
+// Fill positions [-hl, 0) and [N, N+hr) of the LDS level buffer.
+template <typename T>
+__device__ __forceinline__ void fill_halo(T* buf, int N, int hl, int hr, int mode, int npow2,
+                                          const T* hist_b, int hist_len) {
+  const int total = hl + hr;
+  for (int q = threadIdx.x; q < total; q += blockDim.x) {
+    const int idx = q < hl ? q - hl : N + (q - hl);
+    buf[idx] = halo_value_lds(buf, idx, N, mode, npow2, hist_b, hist_len);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Forward: one 16-byte vector of consecutive outputs t0..t0+V-1, both filters from one set of
+// LDS reads.  acc_e (+)= x[t0 + e - i*s] * f[i], i ascending (ScalarOps.java:707-719 order).
+template <typename T, int L, bool FMA, int S>
+__device__ __forceinline__ void fwd_window(const T* buf, int t0, const T* lo, const T* hi,
+                                           T (&al)[VT<T>::V], T (&ah)[VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  constexpr int RU = (((L - 1) * S) + V - 1) / V * V;   // aligned left reach
+  constexpr int NE = RU + V;
+  T w[NE];
+#pragma unroll
+  for (int k = 0; k < NE / V; ++k) {
+    vec v = *reinterpret_cast<const vec*>(buf + t0 - RU + k * V);
+#pragma unroll
+    for (int e = 0; e < V; ++e) w[k * V + e] = v[e];
+  }
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const T xv = w[RU + e - i * S];
+      al[e] = madd<FMA>(al[e], xv, lo[i]);
+      ah[e] = madd<FMA>(ah[e], xv, hi[i]);
+    }
+  }
+}
+
+template <typename T, int L, bool FMA>
+__device__ __forceinline__ void fwd_vec(const T* buf, int t0, int S, const T* lo, const T* hi, int taps,
+                                        T (&al)[VT<T>::V], T (&ah)[VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  if constexpr (L > 0) {
+    if (S == 1) { fwd_window<T, L, FMA, 1>(buf, t0, lo, hi, al, ah); return; }
+    if constexpr (V == 4) {
+      if (S == 2) { fwd_window<T, L, FMA, 2>(buf, t0, lo, hi, al, ah); return; }
+    }
+#pragma unroll
+    for (int i = 0; i < L; ++i) {   // S is a multiple of V: aligned 16-byte reads
+      const vec v = *reinterpret_cast<const vec*>(buf + t0 - i * S);
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        al[e] = madd<FMA>(al[e], v[e], lo[i]);
+        ah[e] = madd<FMA>(ah[e], v[e], hi[i]);
+      }
+    }
+  } else {
+    for (int i = 0; i < taps; ++i) {
+      const T fl = lo[i], fh = hi[i];
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const T xv = buf[t0 + e - i * S];
+        al[e] = madd<FMA>(al[e], xv, fl);
+        ah[e] = madd<FMA>(ah[e], xv, fh);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Inverse, one branch: acc_e (+)= f[i] * buf[t0 + e + dir*i*s + off], i ascending
+// (MultiLevelMODWTTransform.java:578-588 periodic, :612-639 symmetric orientations).
+template <typename T, int L, bool FMA, int S, int DIR>
+__device__ __forceinline__ void inv_window(const T* buf, int base, const T* f, T (&acc)[VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  // DIR=+1: elements [base, base + V-1 + (L-1)S]; DIR=-1: [base - (L-1)S, base + V-1]
+  constexpr int REACH = (L - 1) * S;
+  constexpr int RU = (REACH + V - 1) / V * V;
+  constexpr int NE = RU + V;
+  T w[NE];
+  const int start = DIR > 0 ? base : base - RU;
+#pragma unroll
+  for (int k = 0; k < NE / V; ++k) {
+    vec v = *reinterpret_cast<const vec*>(buf + start + k * V);
+#pragma unroll
+    for (int e = 0; e < V; ++e) w[k * V + e] = v[e];
+  }
+#pragma unroll
+  for (int i = 0; i < L; ++i) {
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      const T xv = DIR > 0 ? w[e + i * S] : w[RU + e - i * S];
+      acc[e] = madd<FMA>(acc[e], xv, f[i]);
+    }
+  }
+}
+
+template <typename T, int L, bool FMA>
+__device__ __forceinline__ void inv_branch(const T* buf, int t0, int S, int dir, int off, const T* f, int taps,
+                                           T (&acc)[VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  if constexpr (L > 0) {
+    if ((off & (V - 1)) == 0) {
+      const int base = t0 + off;
+      if (S == 1) {
+        if (dir > 0) inv_window<T, L, FMA, 1, 1>(buf, base, f, acc);
+        else inv_window<T, L, FMA, 1, -1>(buf, base, f, acc);
+        return;
+      }
+      if constexpr (V == 4) {
+        if (S == 2) {
+          if (dir > 0) inv_window<T, L, FMA, 2, 1>(buf, base, f, acc);
+          else inv_window<T, L, FMA, 2, -1>(buf, base, f, acc);
+          return;
+        }
+      }
+      const int step = dir * S;
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        const vec v = *reinterpret_cast<const vec*>(buf + base + i * step);
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] = madd<FMA>(acc[e], v[e], f[i]);
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = madd<FMA>(acc[e], buf[t0 + e + dir * i * S + off], f[i]);
+    }
+  } else {
+    for (int i = 0; i < taps; ++i) {
+      const T fi = f[i];
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = madd<FMA>(acc[e], buf[t0 + e + dir * i * S + off], fi);
+    }
+  }
+}
+
+// Pairwise inverse: acc_e += (h[i]*a[idx] + g[i]*d[idx])  (MODWTTransform.java:251-252, :265-266,
+// :290-291; MultiLevelMODWTTransform.java:596-597).  idx = t0 + e + dir*i*s.
+template <typename T, bool FMA>
+__device__ __forceinline__ T pair_term(T h, T a, T g, T d) {
+  if constexpr (FMA) return fma_t(h, a, g * d);
+  else return h * a + g * d;
+}
+
+template <typename T, int L, bool FMA>
+__device__ __forceinline__ void inv_pair(const T* A, const T* D, int t0, int S, int dir, const T* h, const T* g,
+                                         int taps, T (&acc)[VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  if constexpr (L > 0) {
+    if (S % V == 0) {
+      const int step = dir * S;
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        const vec va = *reinterpret_cast<const vec*>(A + t0 + i * step);
+        const vec vd = *reinterpret_cast<const vec*>(D + t0 + i * step);
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] = acc[e] + pair_term<T, FMA>(h[i], va[e], g[i], vd[e]);
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < L; ++i) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int idx = t0 + e + dir * i * S;
+        acc[e] = acc[e] + pair_term<T, FMA>(h[i], A[idx], g[i], D[idx]);
+      }
+    }
+  } else {
+    for (int i = 0; i < taps; ++i) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const int idx = t0 + e + dir * i * S;
+        acc[e] = acc[e] + pair_term<T, FMA>(h[i], A[idx], g[i], D[idx]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Global <-> LDS row transfers (16-byte vectors when aligned; scalar + zero tail otherwise).
+template <typename T>
+__device__ __forceinline__ void row_to_lds(T* buf, const T* __restrict__ src, int N, bool vec_ok,
+                                           int validate, unsigned long long* bad, unsigned long long flat0) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  const int nvec = (N + V - 1) / V;
+  for (int w = threadIdx.x; w < nvec; w += blockDim.x) {
+    const int t0 = w * V;
+    vec v;
+    if (vec_ok && t0 + V <= N) {
+      v = __builtin_nontemporal_load(reinterpret_cast<const vec*>(src + t0));
+    } else {
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[e] = (t0 + e < N) ? src[t0 + e] : T(0);
+    }
+    if (validate) {
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if (t0 + e < N && !finite_t(v[e])) atomicMin(bad, flat0 + (unsigned long long)(t0 + e));
+    }
+    *reinterpret_cast<vec*>(buf + t0) = v;
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void store_vec(T* __restrict__ dst, int t0, int N, bool vec_ok, const T (&v)[VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  if (vec_ok && t0 + V <= N) {
+    vec o;
+#pragma unroll
+    for (int e = 0; e < V; ++e) o[e] = v[e];
+    __builtin_nontemporal_store(o, reinterpret_cast<vec*>(dst + t0));
+  } else {
+#pragma unroll
+    for (int e = 0; e < V; ++e)
+      if (t0 + e < N) dst[t0 + e] = v[e];
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void check_out(int validate, unsigned long long* bad, unsigned long long flat0, int t0,
+                                          int N, const T (&v)[VT<T>::V]) {
+  if (!validate) return;
+  constexpr int V = VT<T>::V;
+#pragma unroll
+  for (int e = 0; e < V; ++e)
+    if (t0 + e < N && !finite_t(v[e])) atomicMin(bad, (1ull << 62) | (flat0 + (unsigned long long)(t0 + e)));
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused multi-level forward: MultiLevelMODWTTransform.decompose (:243-251) / BatchSIMDMODWT
+// .batchMultiLevelMODWTSoA (:362-377) / VectorWaveSwtAdapter.decomposeSWT (:370-390) /
+// BatchStreamingMODWT.processMultiLevel (:130-158) for one signal per workgroup.
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(kMaxThreads) k_forward_fused(const FwdArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* buf = reinterpret_cast<T*>(smem) + p.hlpad;
+  const long long b = blockIdx.x;
+  const int N = p.N;
+  const int nvec = (N + V - 1) / V;
+  const int NT = blockDim.x;
+  const int tid = threadIdx.x;
+  const bool vec_ok = p.vec_io != 0;
+  const unsigned long long flat0 = (unsigned long long)b * (unsigned long long)N;
+
+  row_to_lds(buf, p.x + b * p.ldx, N, vec_ok, p.validate, p.bad, flat0);
+
+  T areg[kNV][V];
+  for (int j = 1; j <= p.J; ++j) {
+    const LevelDesc lv = p.lv[j - 1];
+    const T* hist_b = (lv.mode == kHaloHistory) ? p.hist[j - 1] + b * lv.hist_len : nullptr;
+    __syncthreads();  // level input complete in LDS
+    fill_halo(buf, N, lv.hl, lv.hr, lv.mode, p.npow2, hist_b, lv.hist_len);
+    __syncthreads();  // halo complete
+
+    T* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
+    const bool last = (j == p.J);
+#pragma unroll
+    for (int k = 0; k < kNV; ++k) {
+      const int w = tid + k * NT;
+      if (w < nvec) {
+        const int t0 = w * V;
+        T al[V], ah[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) { al[e] = T(0); ah[e] = T(0); }
+        fwd_vec<T, L, FMA>(buf, t0, lv.s, p.lo, p.hi, p.taps, al, ah);
+        store_vec(dout, t0, N, vec_ok, ah);
+        check_out<T>(p.validate, p.bad, flat0, t0, N, ah);
+        if (last) {
+          store_vec(p.approx + b * (size_t)N, t0, N, vec_ok, al);
+          check_out<T>(p.validate, p.bad, flat0, t0, N, al);
+        } else {
+          check_out<T>(p.validate, p.bad, flat0, t0, N, al);
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) areg[k][e] = al[e];
+      }
+    }
+    // Streaming: new left history = last hist_len samples of this level's input
+    // (BatchStreamingMODWT.updateHistoryFromSoA :337-352; buf[<0] holds the old history).
+    if (p.hist_update && lv.hist_len > 0) {
+      T* hnew = p.hist[j - 1] + b * lv.hist_len;
+      for (int q = tid; q < lv.hist_len; q += NT) hnew[q] = buf[q + N - lv.hist_len];
+    }
+    if (!last) {
+      __syncthreads();  // every read of this level's input done
+#pragma unroll
+      for (int k = 0; k < kNV; ++k) {
+        const int w = tid + k * NT;
+        if (w < nvec) {
+          typename VT<T>::v o;
+#pragma unroll
+          for (int e = 0; e < V; ++e) o[e] = areg[k][e];
+          *reinterpret_cast<typename VT<T>::v*>(buf + w * V) = o;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused multi-level inverse: MultiLevelMODWTTransform.reconstruct (:339-349, :554-645),
+// VectorWaveSwtAdapter.reconstructPeriodic (:444-474), MODWTTransform.inverse (J=1, pairwise),
+// with the denoise threshold (MutableMultiLevelMODWTResult.java:97-114) fused into the detail load.
+template <typename T>
+__device__ __forceinline__ T threshold_t(T c, T thr, int soft) {
+  const T av = c < T(0) ? -c : c;
+  if (soft) {
+    if (av > thr) {
+      const T sg = c > T(0) ? T(1) : (c < T(0) ? T(-1) : c);  // Math.signum
+      return sg * (av - thr);
+    }
+    return T(0);
+  }
+  return av <= thr ? T(0) : c;
+}
+
+template <typename T>
+__device__ __forceinline__ void load_row_regs(T (&r)[kNV][VT<T>::V], const T* __restrict__ src, int N, int nvec,
+                                              bool vec_ok, bool zero, const T* thr, T thr_b, int soft) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  const int NT = blockDim.x;
+#pragma unroll
+  for (int k = 0; k < kNV; ++k) {
+    const int w = threadIdx.x + k * NT;
+    if (w < nvec) {
+      const int t0 = w * V;
+      if (zero) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) r[k][e] = T(0);
+      } else if (vec_ok && t0 + V <= N) {
+        const vec v = __builtin_nontemporal_load(reinterpret_cast<const vec*>(src + t0));
+#pragma unroll
+        for (int e = 0; e < V; ++e) r[k][e] = v[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < V; ++e) r[k][e] = (t0 + e < N) ? src[t0 + e] : T(0);
+      }
+      if (thr) {
+#pragma unroll
+        for (int e = 0; e < V; ++e) r[k][e] = threshold_t(r[k][e], thr_b, soft);
+      }
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void regs_to_lds(T* buf, const T (&r)[kNV][VT<T>::V], int nvec) {
+  constexpr int V = VT<T>::V;
+  const int NT = blockDim.x;
+#pragma unroll
+  for (int k = 0; k < kNV; ++k) {
+    const int w = threadIdx.x + k * NT;
+    if (w < nvec) {
+      typename VT<T>::v o;
+#pragma unroll
+      for (int e = 0; e < V; ++e) o[e] = r[k][e];
+      *reinterpret_cast<typename VT<T>::v*>(buf + w * V) = o;
+    }
+  }
+}
+
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(kMaxThreads) k_inverse_fused(const InvArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* A = reinterpret_cast<T*>(smem) + p.hlpad_a;
+  T* D = reinterpret_cast<T*>(smem) + p.region_d + p.hlpad_d;
+  const long long b = blockIdx.x;
+  const int N = p.N;
+  const int nvec = (N + V - 1) / V;
+  const int NT = blockDim.x;
+  const int tid = threadIdx.x;
+  const bool vec_ok = p.vec_io != 0;
+  const T thr_b = p.thr ? p.thr[b] : T(0);
+  const size_t plane = (size_t)p.B * (size_t)N;
+
+  T reg[kNV][V];
+  // coarsest level: approximation -> A, d_J -> D
+  load_row_regs<T>(reg, p.approx + b * (size_t)N, N, nvec, vec_ok, p.approx_zero != 0, nullptr, T(0), 0);
+  regs_to_lds(A, reg, nvec);
+  {
+    const LevelDesc lv = p.lv[p.J - 1];
+    load_row_regs<T>(reg, p.details + (size_t)(p.J - 1) * plane + b * (size_t)N, N, nvec, vec_ok, lv.use_d == 0,
+                  p.thr, thr_b, p.soft);
+    regs_to_lds(D, reg, nvec);
+  }
+
+  for (int j = p.J; j >= 1; --j) {
+    const LevelDesc lv = p.lv[j - 1];
+    __syncthreads();  // A (level-j approximation) and D (d_j) complete
+    fill_halo(A, N, lv.hl, lv.hr, lv.mode, 0, (const T*)nullptr, 0);
+    fill_halo(D, N, lv.hl, lv.hr, lv.mode, 0, (const T*)nullptr, 0);
+    __syncthreads();
+
+    // prefetch d_{j-1} while this level computes (async-stage split)
+    T dnext[kNV][V];
+    if (j > 1) {
+      const LevelDesc ln = p.lv[j - 2];
+      load_row_regs<T>(dnext, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, vec_ok, ln.use_d == 0,
+                    p.thr, thr_b, p.soft);
+    }
+#pragma unroll
+    for (int k = 0; k < kNV; ++k) {
+      const int w = tid + k * NT;
+      if (w < nvec) {
+        const int t0 = w * V;
+        T acc[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[e] = T(0);
+        if (p.pair) {
+          inv_pair<T, L, FMA>(A, D, t0, lv.s, lv.dir_a, p.lo, p.hi, p.taps, acc);
+        } else {
+          inv_branch<T, L, FMA>(A, t0, lv.s, lv.dir_a, lv.off_a, p.lo, p.taps, acc);
+          inv_branch<T, L, FMA>(D, t0, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
+        }
+        if (j == 1) {
+          store_vec(p.y + b * (size_t)N, t0, N, vec_ok, acc);
+        } else {
+#pragma unroll
+          for (int e = 0; e < V; ++e) reg[k][e] = acc[e];
+        }
+      }
+    }
+    if (j > 1) {
+      __syncthreads();  // all reads of A and D done
+      regs_to_lds(A, reg, nvec);
+      regs_to_lds(D, dnext, nvec);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Per-level tiled kernels (signals longer than the fused kernels hold in LDS).  One workgroup per
+// (tile, signal); the tile and its halo are gathered from HBM through the reference's index map.
+template <typename T>
+__device__ __forceinline__ T halo_value_global(const T* __restrict__ src, int idx, int N, int mode, int npow2,
+                                               const T* hist_b, int hist_len) {
+  if (idx >= 0 && idx < N) return src[idx];
+  switch (mode) {
+    case kHaloPeriodic: { int r = idx % N; if (r < 0) r += N; return src[r]; }
+    case kHaloSymmetric: return src[sym_index(idx, N)];
+    case kHaloFftPad: { int r = idx < 0 ? idx + npow2 : idx; return (r >= 0 && r < N) ? src[r] : T(0); }
+    case kHaloHistory: return (idx < 0 && idx >= -hist_len) ? hist_b[hist_len + idx] : T(0);
+    default: return T(0);
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void tile_to_lds(T* buf, const T* __restrict__ src, int N, int ts, int lo_q, int hi_q,
+                                            int mode, int npow2, const T* hist_b, int hist_len, const T* thr,
+                                            T thr_b, int soft, bool zero) {
+  // buf[q] = value at signal index ts + q, q in [lo_q, hi_q)
+  for (int q = lo_q + (int)threadIdx.x; q < hi_q; q += blockDim.x) {
+    T v = zero ? T(0) : halo_value_global(src, ts + q, N, mode, npow2, hist_b, hist_len);
+    if (thr) v = threshold_t(v, thr_b, soft);
+    buf[q] = v;
+  }
+}
+
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(256) k_forward_level(const LevelArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* buf = reinterpret_cast<T*>(smem) + p.hlpad;
+  const long long b = blockIdx.y;
+  const int N = p.N;
+  const int ts = blockIdx.x * p.tile;
+  const int cnt = min(p.tile, N - ts);
+  const int nv = (cnt + V - 1) / V;
+  const LevelDesc lv = p.lv;
+  const T* src = p.src_a + b * p.lda;
+  const T* hist_b = (lv.mode == kHaloHistory) ? p.hist + b * lv.hist_len : nullptr;
+  tile_to_lds(buf, src, N, ts, -lv.hl, nv * V, lv.mode, p.npow2, hist_b, lv.hist_len, (const T*)nullptr, T(0), 0,
+              false);
+  if (p.validate) {
+    for (int q = threadIdx.x; q < cnt; q += blockDim.x)
+      if (!finite_t(buf[q])) atomicMin(p.bad, (unsigned long long)b * N + ts + q);
+  }
+  __syncthreads();
+  const bool vec_ok = p.vec_io != 0;  // rows 16-B aligned (tile starts are multiples of V)
+  for (int w = threadIdx.x; w < nv; w += blockDim.x) {
+    const int t0 = w * V;
+    T al[V], ah[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { al[e] = T(0); ah[e] = T(0); }
+    fwd_vec<T, L, FMA>(buf, t0, lv.s, p.lo, p.hi, p.taps, al, ah);
+    store_vec(p.out_a + b * (size_t)N + ts, t0, cnt, vec_ok, al);
+    store_vec(p.out_d + b * (size_t)N + ts, t0, cnt, vec_ok, ah);
+    check_out<T>(p.validate, p.bad, (unsigned long long)b * N + ts, t0, cnt, al);
+    check_out<T>(p.validate, p.bad, (unsigned long long)b * N + ts, t0, cnt, ah);
+  }
+}
+
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(256) k_inverse_level(const LevelArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* A = reinterpret_cast<T*>(smem) + p.hlpad;
+  T* D = reinterpret_cast<T*>(smem) + p.region_d + p.hlpad_d;
+  const long long b = blockIdx.y;
+  const int N = p.N;
+  const int ts = blockIdx.x * p.tile;
+  const int cnt = min(p.tile, N - ts);
+  const int nv = (cnt + V - 1) / V;
+  const LevelDesc lv = p.lv;
+  const T thr_b = p.thr ? p.thr[b] : T(0);
+  const int span = nv * V;
+  tile_to_lds(A, p.src_a + b * (size_t)N, N, ts, -lv.hl, span + lv.hr, lv.mode, 0, (const T*)nullptr, 0,
+              (const T*)nullptr, T(0), 0, p.src_a == nullptr);
+  tile_to_lds(D, p.src_d + b * (size_t)N, N, ts, -lv.hl, span + lv.hr, lv.mode, 0, (const T*)nullptr, 0, p.thr,
+              thr_b, p.soft, p.use_d == 0 || p.src_d == nullptr);
+  __syncthreads();
+  const bool vec_ok = p.vec_io != 0;
+  for (int w = threadIdx.x; w < nv; w += blockDim.x) {
+    const int t0 = w * V;
+    T acc[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) acc[e] = T(0);
+    if (p.pair) {
+      inv_pair<T, L, FMA>(A, D, t0, lv.s, lv.dir_a, p.lo, p.hi, p.taps, acc);
+    } else {
+      inv_branch<T, L, FMA>(A, t0, lv.s, lv.dir_a, lv.off_a, p.lo, p.taps, acc);
+      inv_branch<T, L, FMA>(D, t0, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
+    }
+    store_vec(p.out_a + b * (size_t)N + ts, t0, cnt, vec_ok, acc);
+  }
+}
+
+template <typename T>
+__global__ void k_history_update(const T* __restrict__ in, long long ld_in, const T* __restrict__ old_hist,
+                                 T* __restrict__ new_hist, int n, int hist_len) {
+  const long long b = blockIdx.y;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= hist_len) return;
+  const int q = p + n - hist_len;
+  new_hist[b * hist_len + p] = q >= 0 ? in[b * ld_in + q] : old_hist[b * hist_len + p + n];
+}
+
+// ---------------------------------------------------------------------------------------------
+// VectorWaveSwtAdapter.estimateNoiseSigma (:627-645): exact median of |c| by MSB-first radix
+// selection on the IEEE bit patterns (non-negative doubles order as unsigned integers), then
+// sigma = median / 0.6745 and the universal threshold T = sigma * sqrt(2 ln N) (:514).
+#ifdef VW_MISC_UNIT
+constexpr int kSigmaThreads = 1024;
+constexpr int kSigmaKeys = 16;
+
+__device__ __forceinline__ unsigned long long abs_bits(double v) {
+  return (unsigned long long)__double_as_longlong(v) & 0x7FFFFFFFFFFFFFFFull;
+}
+
+__global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __restrict__ coeffs, long long ld, int N,
+                                                               double scale_c, double* sigma_out, double* thr_out) {
+  __shared__ unsigned int hist[2][256];
+  __shared__ unsigned int wsum[2][kSigmaThreads / 64];
+  __shared__ unsigned long long prefix[2];
+  __shared__ long long krem[2];
+  const long long b = blockIdx.x;
+  const double* c = coeffs + b * ld;
+  const int tid = threadIdx.x;
+  const int nsel = (N % 2 == 0) ? 2 : 1;
+  const bool in_regs = N <= kSigmaThreads * kSigmaKeys;
+  unsigned long long keys[kSigmaKeys];
+  if (in_regs) {
+#pragma unroll
+    for (int k = 0; k < kSigmaKeys; ++k) {
+      const int i = tid + k * kSigmaThreads;
+      keys[k] = i < N ? abs_bits(c[i]) : 0ull;
+    }
+  }
+  if (tid == 0) {
+    prefix[0] = prefix[1] = 0ull;
+    krem[0] = (N % 2 == 0) ? N / 2 - 1 : N / 2;
+    krem[1] = N / 2;
+  }
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int q = tid; q < 512; q += kSigmaThreads) hist[q >> 8][q & 255] = 0u;
+    __syncthreads();
+    const unsigned long long hm = (shift == 56) ? 0ull : (~0ull << (shift + 8));
+    const unsigned long long p0 = prefix[0], p1 = prefix[1];
+    if (in_regs) {
+#pragma unroll
+      for (int k = 0; k < kSigmaKeys; ++k) {
+        const int i = tid + k * kSigmaThreads;
+        if (i < N) {
+          const unsigned long long key = keys[k];
+          const unsigned d = (unsigned)(key >> shift) & 255u;
+          if (((key ^ p0) & hm) == 0) atomicAdd(&hist[0][d], 1u);
+          if (nsel == 2 && ((key ^ p1) & hm) == 0) atomicAdd(&hist[1][d], 1u);
+        }
+      }
+    } else {
+      for (int i = tid; i < N; i += kSigmaThreads) {
+        const unsigned long long key = abs_bits(c[i]);
+        const unsigned d = (unsigned)(key >> shift) & 255u;
+        if (((key ^ p0) & hm) == 0) atomicAdd(&hist[0][d], 1u);
+        if (nsel == 2 && ((key ^ p1) & hm) == 0) atomicAdd(&hist[1][d], 1u);
+      }
+    }
+    __syncthreads();
+    // exclusive scan of 2 x 256 bins by threads 0..511 (wave-level shuffles)
+    const int r = tid >> 8, bin = tid & 255, lane = tid & 63, wv = (tid >> 6) & 3;
+    unsigned incl = 0;
+    if (tid < 512) {
+      const unsigned h = hist[r][bin];
+      incl = h;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      if (lane == 63) wsum[r][wv] = incl;
+    }
+    __syncthreads();
+    if (tid < 512 && r < nsel) {
+      unsigned base = 0;
+      for (int q = 0; q < wv; ++q) base += wsum[r][q];
+      const unsigned h = hist[r][bin];
+      const unsigned long long excl = (unsigned long long)(base + incl - h);
+      const long long k = krem[r];
+      if ((long long)excl <= k && k < (long long)(excl + h)) {
+        prefix[r] |= ((unsigned long long)bin) << shift;
+        krem[r] = k - (long long)excl;
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const double v1 = __longlong_as_double((long long)prefix[0]);
+    const double v2 = __longlong_as_double((long long)prefix[1]);
+    const double median = (nsel == 2) ? (v1 + v2) / 2.0 : v1;
+    const double sigma = median / 0.6745;
+    if (sigma_out) sigma_out[b] = sigma;
+    if (thr_out) thr_out[b] = sigma * scale_c;
+  }
+}
+
+#endif  // VW_MISC_UNIT
+
+template <typename T>
+__global__ void k_threshold(T* c, long long B, long long N, const T* __restrict__ thr, int soft) {
+  const long long total = B * N;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long b = i / N;
+    c[i] = threshold_t(c[i], thr[b], soft);
+  }
+}
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+template <typename T>
+__global__ void k_fill_uniform(T* x, long long count, unsigned long long seed, long long offset) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < count;
+       i += (long long)gridDim.x * blockDim.x) {
+    const unsigned long long r = splitmix64(seed ^ (unsigned long long)(offset + i));
+    const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
+    x[i] = (T)(2.0 * u - 1.0);
+  }
+}
+
+// BatchSIMDMODWT.haarBatchMODWTSoA (:86-140): hard-coded 0.5 / -0.5 taps.
+template <typename T>
+__global__ void k_single_haar_batch(const T* __restrict__ x, long long ldx, int N, T* approx, T* detail) {
+  const long long b = blockIdx.y;
+  for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < N; t += gridDim.x * blockDim.x) {
+    const int tm1 = (t - 1 + N) % N;
+    const T s0 = x[b * ldx + t], s1 = x[b * ldx + tm1];
+    approx[b * (size_t)N + t] = s0 * T(0.5) + s1 * T(0.5);
+    detail[b * (size_t)N + t] = s0 * T(0.5) + s1 * T(-0.5);
+  }
+}
+
+
+}  // namespace vw

@@ -1,0 +1,136 @@
+// vw_internal.h -- shared between the HIP kernels (vw_kernels.hip) and the C-ABI host layer
+// (vw_capi.cpp).  Not installed; the public boundary is include/vectorwave_amd.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace vw {
+
+constexpr int kMaxTaps = 64;    // longest base filter accepted (COIF10 = 60 taps)
+constexpr int kMaxLevels = 24;  // batch semantics have no level cap; LDS / N bound it in practice
+constexpr int kNV = 8;          // vectors (16 B each) held per thread in the fused kernels
+constexpr int kMaxThreads = 1024;
+constexpr int kLdsBytes = 160 * 1024;
+
+// Source of the values outside [0, N) of a level's input ("halo"), i.e. the reference's index map.
+enum HaloMode : int {
+  kHaloPeriodic = 0,   // ((i % N) + N) % N        ScalarOps.java:700-723, (t+l)%N in the inverses
+  kHaloZero = 1,       // 0                        ScalarOps.java:790-808, :590-601
+  kHaloSymmetric = 2,  // MathUtils.symmetricBoundaryExtension  core/util/MathUtils.java:30-51
+  kHaloFftPad = 3,     // i + nextPow2(N) if < N else 0 (FFT branch zero-pads)  ScalarOps.java:650-675
+  kHaloHistory = 4     // streaming left history   BatchSIMDMODWT.java:447-507
+};
+
+// Per-level description, computed on the host (vw_capi.cpp) from the reference's bookkeeping.
+struct LevelDesc {
+  int s;        // a-trous spacing 2^(j-1)
+  int hl, hr;   // halo extents (elements) the level reads left of 0 / right of N-1
+  int mode;     // HaloMode of the level input (forward) / of both inverse inputs
+  int dir_a;    // inverse approx branch: +1 reads t + i*s + off_a, -1 reads t - i*s + off_a
+  int off_a;
+  int dir_d;    // inverse detail branch
+  int off_d;
+  int use_d;    // inverse: 1 = d_j from memory, 0 = zero details (reconstructFromLevel / Levels)
+  int hist_len; // streaming: left history length of this level (L_j - 1)
+};
+
+template <typename T>
+struct FwdArgs {
+  const T* x;           // [B][ldx]
+  long long ldx;
+  T* details;           // [J][B][N]
+  T* approx;            // [B][N]
+  long long B;
+  int N;
+  int J;
+  int npow2;            // nextPow2(N) for kHaloFftPad
+  int hlpad;            // LDS offset of element 0 (multiple of the vector width)
+  int vec_io;           // 1: rows and outputs are 16-B aligned -> vector global I/O
+  int validate;         // 1: non-finite check on input and outputs (atomicMin into *bad)
+  unsigned long long* bad;
+  // streaming history (kHaloHistory): hist[j] is [B][hist_len_j], oldest first
+  T* hist[kMaxLevels];
+  int hist_update;      // 1: write the new history after each level
+  int taps;             // L (runtime copy; kernels are also templated on it)
+  T lo[kMaxTaps];       // base taps * 1/sqrt(2)  (ScalarOps.java:909-916: same at every level)
+  T hi[kMaxTaps];
+  LevelDesc lv[kMaxLevels];
+};
+
+template <typename T>
+struct InvArgs {
+  const T* details;     // [J][B][N]
+  const T* approx;      // [B][N]
+  T* y;                 // [B][N]
+  long long B;
+  int N;
+  int J;
+  int hlpad_a, hlpad_d; // LDS offsets of element 0 in the A and D regions
+  int region_d;         // element offset of the D region start in LDS
+  int vec_io;
+  int pair;             // 1: sum += (h*a + g*d) per tap (MODWTTransform.inverse, ZERO multi-level)
+  int approx_zero;
+  const T* thr;         // per-signal threshold [B] (nullptr = no thresholding)
+  int soft;
+  int taps;
+  T lo[kMaxTaps];
+  T hi[kMaxTaps];
+  LevelDesc lv[kMaxLevels];
+};
+
+// Per-level tiled fallback (N too large for the fused kernels): one launch per level.
+template <typename T>
+struct LevelArgs {
+  const T* src_a;       // forward: level input [B][lda]; inverse: approx input [B][N]
+  long long lda;
+  const T* src_d;       // inverse: details of this level [B][N]
+  T* out_a;             // forward: approx out [B][N]; inverse: y out [B][N]
+  T* out_d;             // forward: detail out [B][N]
+  const T* hist;        // kHaloHistory source [B][hist_len]
+  long long B;
+  int N;
+  int tile;             // outputs per workgroup
+  int hlpad;            // LDS offset of tile element 0 (A)
+  int region_d, hlpad_d;
+  int pair;
+  const T* thr;
+  int soft;
+  int use_d;
+  int vec_io;
+  int validate;
+  unsigned long long* bad;
+  int npow2;
+  int taps;
+  T lo[kMaxTaps];
+  T hi[kMaxTaps];
+  LevelDesc lv;
+};
+
+// Launchers (vw_kernels.hip).  Return hipSuccess or the launch error.
+template <typename T>
+hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, hipStream_t st);
+template <typename T>
+hipError_t launch_inverse_fused(const InvArgs<T>& a, int threads, int lds_bytes, bool fma, hipStream_t st);
+template <typename T>
+hipError_t launch_forward_level(const LevelArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
+template <typename T>
+hipError_t launch_inverse_level(const LevelArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
+template <typename T>
+hipError_t launch_history_update(const T* level_in, long long ld_in, const T* old_hist, T* new_hist,
+                                 long long B, int n, int hist_len, hipStream_t st);
+
+hipError_t launch_noise_sigma(const double* coeffs, long long ld, long long B, int N, double scale_c,
+                              double* sigma_out, double* thr_out, hipStream_t st);
+template <typename T>
+hipError_t launch_threshold(T* c, long long B, long long N, const T* thr, int soft, hipStream_t st);
+template <typename T>
+hipError_t launch_fill_uniform(T* x, long long count, unsigned long long seed, long long offset, hipStream_t st);
+template <typename T>
+hipError_t launch_single_haar_batch(const T* x, long long ldx, long long B, int N, T* approx, T* detail,
+                                    hipStream_t st);
+
+// Which compile-time tap counts have unrolled kernels; others use the runtime-L kernel.
+bool has_unrolled_taps(int L);
+int fused_max_threads();
+
+}  // namespace vw

@@ -1,0 +1,44 @@
+#define VW_T double
+// vw_inv_f64.hip -- launchers (instantiation unit) for the kernels in vw_device.h.
+#include "vw_device.h"
+
+namespace vw {
+
+#define VW_TAP_LIST(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(24) X(30)
+
+// Raise the dynamic-LDS limit once per kernel instantiation (a call per launch costs host time).
+// `configured` must be a static of the caller, which is unique per kernel instantiation.
+template <typename Kern>
+static hipError_t set_lds(Kern k, int lds_bytes, int* configured) {
+  if (lds_bytes > *configured) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       kLdsBytes);
+    if (e != hipSuccess) return e;
+    *configured = kLdsBytes;
+  }
+  return hipSuccess;
+}
+
+template <typename T, int L, bool FMA>
+static hipError_t run_inverse_fused(const InvArgs<T>& a, int threads, int lds, hipStream_t st) {
+  auto k = k_inverse_fused<T, L, FMA>;
+  static int configured = 64 * 1024;
+  hipError_t e = set_lds(k, lds, &configured);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(threads), lds, st, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_inverse_fused(const InvArgs<T>& a, int threads, int lds, bool fma, hipStream_t st) {
+  switch (a.taps) {
+#define VW_CASE(n) \
+    case n: return fma ? run_inverse_fused<T, n, true>(a, threads, lds, st) : run_inverse_fused<T, n, false>(a, threads, lds, st);
+    VW_TAP_LIST(VW_CASE)
+#undef VW_CASE
+    default:
+      return fma ? run_inverse_fused<T, 0, true>(a, threads, lds, st) : run_inverse_fused<T, 0, false>(a, threads, lds, st);
+  }
+}
+template hipError_t launch_inverse_fused<VW_T>(const InvArgs<VW_T>&, int, int, bool, hipStream_t);
+}  // namespace vw

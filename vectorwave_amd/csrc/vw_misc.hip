@@ -1,0 +1,82 @@
+// vw_misc.hip -- launchers (instantiation unit) for the kernels in vw_device.h.
+#define VW_MISC_UNIT 1
+#include "vw_device.h"
+
+namespace vw {
+
+#define VW_TAP_LIST(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(24) X(30)
+
+// Raise the dynamic-LDS limit once per kernel instantiation (a call per launch costs host time).
+// `configured` must be a static of the caller, which is unique per kernel instantiation.
+template <typename Kern>
+static hipError_t set_lds(Kern k, int lds_bytes, int* configured) {
+  if (lds_bytes > *configured) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       kLdsBytes);
+    if (e != hipSuccess) return e;
+    *configured = kLdsBytes;
+  }
+  return hipSuccess;
+}
+
+bool has_unrolled_taps(int L) {
+  switch (L) {
+#define VW_CASE(n) case n: return true;
+    VW_TAP_LIST(VW_CASE)
+#undef VW_CASE
+    default: return false;
+  }
+}
+
+int fused_max_threads() { return kMaxThreads; }
+
+template <typename T>
+hipError_t launch_history_update(const T* in, long long ld_in, const T* old_hist, T* new_hist, long long B, int n,
+                                 int hist_len, hipStream_t st) {
+  if (hist_len <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_history_update<T>, dim3((unsigned)((hist_len + 255) / 256), (unsigned)B), dim3(256), 0, st,
+                     in, ld_in, old_hist, new_hist, n, hist_len);
+  return hipGetLastError();
+}
+
+hipError_t launch_noise_sigma(const double* coeffs, long long ld, long long B, int N, double scale_c,
+                              double* sigma_out, double* thr_out, hipStream_t st) {
+  hipLaunchKernelGGL(k_noise_sigma, dim3((unsigned)B), dim3(kSigmaThreads), 0, st, coeffs, ld, N, scale_c, sigma_out,
+                     thr_out);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_threshold(T* c, long long B, long long N, const T* thr, int soft, hipStream_t st) {
+  const long long total = B * N;
+  const unsigned grid = (unsigned)std::min<long long>((total + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_threshold<T>, dim3(grid), dim3(256), 0, st, c, B, N, thr, soft);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_fill_uniform(T* x, long long count, unsigned long long seed, long long offset, hipStream_t st) {
+  const unsigned grid = (unsigned)std::min<long long>((count + 255) / 256, 65536);
+  hipLaunchKernelGGL(k_fill_uniform<T>, dim3(grid), dim3(256), 0, st, x, count, seed, offset);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_single_haar_batch(const T* x, long long ldx, long long B, int N, T* approx, T* detail,
+                                    hipStream_t st) {
+  const unsigned gx = (unsigned)std::min(std::max((N + 255) / 256, 1), 1024);
+  hipLaunchKernelGGL(k_single_haar_batch<T>, dim3(gx, (unsigned)B), dim3(256), 0, st, x, ldx, N, approx, detail);
+  return hipGetLastError();
+}
+
+#define VW_INST(T)                                                                                              \
+  template hipError_t launch_history_update<T>(const T*, long long, const T*, T*, long long, int, int,         \
+                                               hipStream_t);                                                    \
+  template hipError_t launch_threshold<T>(T*, long long, long long, const T*, int, hipStream_t);               \
+  template hipError_t launch_fill_uniform<T>(T*, long long, unsigned long long, long long, hipStream_t);       \
+  template hipError_t launch_single_haar_batch<T>(const T*, long long, long long, int, T*, T*, hipStream_t);
+VW_INST(double)
+VW_INST(float)
+#undef VW_INST
+
+}  // namespace vw
