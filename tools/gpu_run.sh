@@ -1,0 +1,37 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel trace.  Each GPU step has its own
+# time limit; a crash/abort/timeout (exit >= 124 or 134/139) stops the script, a plain test failure
+# (exit 1) does not.
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+STEPS="${STEPS:-tests smoke bench prof}"
+fatal() { local rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139 ]; }
+for s in $STEPS; do
+  case "$s" in
+    tests)
+      timeout -k 10 ${T_TESTS:-420} python -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+      tail -5 gpurun_out/pytest_gpu.log; echo "tests rc=$rc" ;;
+    smoke)
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
+      tail -3 gpurun_out/smoke.log; echo "smoke rc=$rc" ;;
+    bench)
+      timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; rc=$?
+      tail -3 gpurun_out/bench.log; echo "bench rc=$rc" ;;
+    ab)  # quick variants: exact/fma, NV 4/8 (no CPU baseline)
+      : > gpurun_out/ab.log
+      for v in "VW_NV=4" "VW_NV=8" "VW_NV=4 FMA=--fma" "VW_NV=8 FMA=--fma"; do
+        env $v bash -c 'timeout -k 10 120 python bench.py --no-cpu-baseline --steps 30 $FMA' >> gpurun_out/ab.log 2>&1; rc=$?
+        echo "$v rc=$rc" >> gpurun_out/ab.log
+        fatal $rc && break
+      done
+      grep -o '"value": [0-9.]*\|"kernels_ms": {[^}]*}\|VW_NV.*' gpurun_out/ab.log ;;
+    prof)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1; rc=$?
+      tail -3 gpurun_out/prof.log; echo "prof rc=$rc" ;;
+    *) echo "unknown step $s"; rc=0 ;;
+  esac
+  if fatal $rc; then echo "fatal rc=$rc at step $s, stopping"; exit $rc; fi
+done
+exit 0

@@ -382,13 +382,18 @@ static vw_status report_bad(unsigned long long bad, int64_t N) {
               (long long)(flat / (unsigned long long)N));
 }
 
-// Plan of a fused launch: threads, LDS bytes.
-static bool fused_plan(int64_t N, int V, int elem, int64_t lds_elems_extra, int* threads, int* lds) {
+// Plan of a fused launch: threads, vectors per thread (4 or 8), LDS bytes.  NV = 4 keeps the
+// per-thread register arrays small (no spills); NV = 8 reaches N = 1024 * 8 * V.
+static bool fused_plan(int64_t N, int V, int elem, int64_t lds_elems_extra, int* threads, int* nv, int* lds) {
   const int64_t nvec = (N + V - 1) / V;
-  int64_t th = round_up((nvec + kNV - 1) / kNV, 64);
+  int want = 4;
+  if (const char* e = getenv("VW_NV")) want = atoi(e) <= 4 ? 4 : 8;
+  if (round_up((nvec + want - 1) / want, 64) > kMaxThreads) want = 8;
+  int64_t th = round_up((nvec + want - 1) / want, 64);
   th = std::max<int64_t>(th, 64);
   if (const char* e = getenv("VW_MIN_THREADS")) th = std::max<int64_t>(th, atoi(e));
   if (th > kMaxThreads) return false;
+  *nv = want;
   const int64_t bytes = lds_elems_extra * elem;
   if (bytes > kLdsBytes) return false;
   *threads = (int)th;
@@ -434,9 +439,9 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
   }
 
   const int hlpad = (int)round_up(max_hl, V);
-  int threads = 0, lds = 0;
+  int threads = 0, lds = 0, nv = 4;
   const int64_t lds_elems = hlpad + nvec * V + V;
-  if (J <= kMaxLevels && fused_plan(N, V, sizeof(T), lds_elems, &threads, &lds) && !getenv("VW_FORCE_TILED")) {
+  if (J <= kMaxLevels && fused_plan(N, V, sizeof(T), lds_elems, &threads, &nv, &lds) && !getenv("VW_FORCE_TILED")) {
     FwdArgs<T> a;
     memset(&a, 0, sizeof(a));
     a.x = x; a.ldx = ldx; a.details = details; a.approx = approx; a.B = B; a.N = (int)N; a.J = J;
@@ -452,7 +457,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     if (validate) VW_HIP(hipMemsetAsync(c->bad, 0xFF, sizeof(unsigned long long), c->stream));
     {
       LaunchTimer lt(c, "forward");
-      hipError_t e = launch_forward_fused<T>(a, threads, lds, fma, c->stream);
+      hipError_t e = launch_forward_fused<T>(a, threads, lds, fma, nv, c->stream);
       if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward launch failed: %s", hipGetErrorString(e));
     }
   } else {
@@ -547,8 +552,8 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   }
   const int hlpad = (int)round_up(max_hl, V);
   const int64_t region = round_up(hlpad + nvec * V + max_hr + V, V);
-  int threads = 0, lds = 0;
-  if (fused_plan(N, V, sizeof(T), 2 * region, &threads, &lds) && !getenv("VW_FORCE_TILED")) {
+  int threads = 0, lds = 0, nv = 4;
+  if (fused_plan(N, V, sizeof(T), 2 * region, &threads, &nv, &lds) && !getenv("VW_FORCE_TILED")) {
     InvArgs<T> a;
     memset(&a, 0, sizeof(a));
     a.details = details; a.approx = approx; a.y = y; a.B = B; a.N = (int)N; a.J = J;
@@ -559,7 +564,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     copy_taps(a.hi, hi, L);
     for (int j = 0; j < J; ++j) a.lv[j] = lv[j];
     LaunchTimer lt(c, "inverse");
-    hipError_t e = launch_inverse_fused<T>(a, threads, lds, fma, c->stream);
+    hipError_t e = launch_inverse_fused<T>(a, threads, lds, fma, nv, c->stream);
     if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse launch failed: %s", hipGetErrorString(e));
   } else {
     const int tile_max = 256 * kNV * V;

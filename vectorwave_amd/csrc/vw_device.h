@@ -58,6 +58,17 @@ __device__ __forceinline__ int sym_index(int idx, int n) {
   return idx;
 }
 
+// Workgroup barrier that orders LDS only: waits for this wave's LDS operations (lgkmcnt(0)) and
+// lets global stores and prefetch loads stay in flight across it.  (__syncthreads() also waits
+// vmcnt(0), which would expose the latency of every detail-level store at every level.)  Values
+// loaded from global memory are waited for by the compiler at their first use, as usual.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt untouched
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 // Value of a level input at signal index idx outside [0, N), read from the LDS copy `buf`
 // (element 0 at buf[0]).  The reference's index maps; see HaloMode.
 template <typename T>
@@ -72,14 +83,23 @@ __device__ __forceinline__ T halo_value_lds(const T* buf, int idx, int N, int mo
   }
 }
 
-// Fill positions [-hl, 0) and [N, N+hr) of the LDS level buffer.
+// Fill positions [-hl, 0) and [N, N+hr) of the LDS level buffer.  The streaming-history fill is a
+// separate loop: it is the only global load inside the level loop, and vmcnt is in order (stores
+// count too), so waiting for it would also wait for every detail store still in flight.
 template <typename T>
 __device__ __forceinline__ void fill_halo(T* buf, int N, int hl, int hr, int mode, int npow2,
                                           const T* hist_b, int hist_len) {
   const int total = hl + hr;
+  if (mode == kHaloHistory) {
+    for (int q = threadIdx.x; q < total; q += blockDim.x) {
+      const int idx = q < hl ? q - hl : N + (q - hl);
+      buf[idx] = (idx < 0 && idx >= -hist_len) ? hist_b[hist_len + idx] : T(0);
+    }
+    return;
+  }
   for (int q = threadIdx.x; q < total; q += blockDim.x) {
     const int idx = q < hl ? q - hl : N + (q - hl);
-    buf[idx] = halo_value_lds(buf, idx, N, mode, npow2, hist_b, hist_len);
+    buf[idx] = halo_value_lds(buf, idx, N, mode, npow2, (const T*)nullptr, 0);
   }
 }
 
@@ -315,7 +335,7 @@ __device__ __forceinline__ void check_out(int validate, unsigned long long* bad,
 // Fused multi-level forward: MultiLevelMODWTTransform.decompose (:243-251) / BatchSIMDMODWT
 // .batchMultiLevelMODWTSoA (:362-377) / VectorWaveSwtAdapter.decomposeSWT (:370-390) /
 // BatchStreamingMODWT.processMultiLevel (:130-158) for one signal per workgroup.
-template <typename T, int L, bool FMA>
+template <typename T, int L, bool FMA, int NV>
 __global__ void __launch_bounds__(kMaxThreads) k_forward_fused(const FwdArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -330,18 +350,18 @@ __global__ void __launch_bounds__(kMaxThreads) k_forward_fused(const FwdArgs<T> 
 
   row_to_lds(buf, p.x + b * p.ldx, N, vec_ok, p.validate, p.bad, flat0);
 
-  T areg[kNV][V];
+  T areg[NV][V];
   for (int j = 1; j <= p.J; ++j) {
     const LevelDesc lv = p.lv[j - 1];
     const T* hist_b = (lv.mode == kHaloHistory) ? p.hist[j - 1] + b * lv.hist_len : nullptr;
-    __syncthreads();  // level input complete in LDS
+    lds_barrier();  // level input complete in LDS
     fill_halo(buf, N, lv.hl, lv.hr, lv.mode, p.npow2, hist_b, lv.hist_len);
-    __syncthreads();  // halo complete
+    lds_barrier();  // halo complete
 
     T* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
     const bool last = (j == p.J);
 #pragma unroll
-    for (int k = 0; k < kNV; ++k) {
+    for (int k = 0; k < NV; ++k) {
       const int w = tid + k * NT;
       if (w < nvec) {
         const int t0 = w * V;
@@ -368,9 +388,9 @@ __global__ void __launch_bounds__(kMaxThreads) k_forward_fused(const FwdArgs<T> 
       for (int q = tid; q < lv.hist_len; q += NT) hnew[q] = buf[q + N - lv.hist_len];
     }
     if (!last) {
-      __syncthreads();  // every read of this level's input done
+      lds_barrier();  // every read of this level's input done
 #pragma unroll
-      for (int k = 0; k < kNV; ++k) {
+      for (int k = 0; k < NV; ++k) {
         const int w = tid + k * NT;
         if (w < nvec) {
           typename VT<T>::v o;
@@ -400,14 +420,14 @@ __device__ __forceinline__ T threshold_t(T c, T thr, int soft) {
   return av <= thr ? T(0) : c;
 }
 
-template <typename T>
-__device__ __forceinline__ void load_row_regs(T (&r)[kNV][VT<T>::V], const T* __restrict__ src, int N, int nvec,
+template <typename T, int NV>
+__device__ __forceinline__ void load_row_regs(T (&r)[NV][VT<T>::V], const T* __restrict__ src, int N, int nvec,
                                               bool vec_ok, bool zero, const T* thr, T thr_b, int soft) {
   constexpr int V = VT<T>::V;
   using vec = typename VT<T>::v;
   const int NT = blockDim.x;
 #pragma unroll
-  for (int k = 0; k < kNV; ++k) {
+  for (int k = 0; k < NV; ++k) {
     const int w = threadIdx.x + k * NT;
     if (w < nvec) {
       const int t0 = w * V;
@@ -430,12 +450,12 @@ __device__ __forceinline__ void load_row_regs(T (&r)[kNV][VT<T>::V], const T* __
   }
 }
 
-template <typename T>
-__device__ __forceinline__ void regs_to_lds(T* buf, const T (&r)[kNV][VT<T>::V], int nvec) {
+template <typename T, int NV>
+__device__ __forceinline__ void regs_to_lds(T* buf, const T (&r)[NV][VT<T>::V], int nvec) {
   constexpr int V = VT<T>::V;
   const int NT = blockDim.x;
 #pragma unroll
-  for (int k = 0; k < kNV; ++k) {
+  for (int k = 0; k < NV; ++k) {
     const int w = threadIdx.x + k * NT;
     if (w < nvec) {
       typename VT<T>::v o;
@@ -446,7 +466,7 @@ __device__ __forceinline__ void regs_to_lds(T* buf, const T (&r)[kNV][VT<T>::V],
   }
 }
 
-template <typename T, int L, bool FMA>
+template <typename T, int L, bool FMA, int NV>
 __global__ void __launch_bounds__(kMaxThreads) k_inverse_fused(const InvArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -461,33 +481,33 @@ __global__ void __launch_bounds__(kMaxThreads) k_inverse_fused(const InvArgs<T> 
   const T thr_b = p.thr ? p.thr[b] : T(0);
   const size_t plane = (size_t)p.B * (size_t)N;
 
-  T reg[kNV][V];
+  T reg[NV][V];
   // coarsest level: approximation -> A, d_J -> D
-  load_row_regs<T>(reg, p.approx + b * (size_t)N, N, nvec, vec_ok, p.approx_zero != 0, nullptr, T(0), 0);
+  load_row_regs<T, NV>(reg, p.approx + b * (size_t)N, N, nvec, vec_ok, p.approx_zero != 0, nullptr, T(0), 0);
   regs_to_lds(A, reg, nvec);
   {
     const LevelDesc lv = p.lv[p.J - 1];
-    load_row_regs<T>(reg, p.details + (size_t)(p.J - 1) * plane + b * (size_t)N, N, nvec, vec_ok, lv.use_d == 0,
+    load_row_regs<T, NV>(reg, p.details + (size_t)(p.J - 1) * plane + b * (size_t)N, N, nvec, vec_ok, lv.use_d == 0,
                   p.thr, thr_b, p.soft);
     regs_to_lds(D, reg, nvec);
   }
 
   for (int j = p.J; j >= 1; --j) {
     const LevelDesc lv = p.lv[j - 1];
-    __syncthreads();  // A (level-j approximation) and D (d_j) complete
+    lds_barrier();  // A (level-j approximation) and D (d_j) complete
     fill_halo(A, N, lv.hl, lv.hr, lv.mode, 0, (const T*)nullptr, 0);
     fill_halo(D, N, lv.hl, lv.hr, lv.mode, 0, (const T*)nullptr, 0);
-    __syncthreads();
+    lds_barrier();
 
     // prefetch d_{j-1} while this level computes (async-stage split)
-    T dnext[kNV][V];
+    T dnext[NV][V];
     if (j > 1) {
       const LevelDesc ln = p.lv[j - 2];
-      load_row_regs<T>(dnext, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, vec_ok, ln.use_d == 0,
+      load_row_regs<T, NV>(dnext, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, vec_ok, ln.use_d == 0,
                     p.thr, thr_b, p.soft);
     }
 #pragma unroll
-    for (int k = 0; k < kNV; ++k) {
+    for (int k = 0; k < NV; ++k) {
       const int w = tid + k * NT;
       if (w < nvec) {
         const int t0 = w * V;
@@ -509,7 +529,7 @@ __global__ void __launch_bounds__(kMaxThreads) k_inverse_fused(const InvArgs<T> 
       }
     }
     if (j > 1) {
-      __syncthreads();  // all reads of A and D done
+      lds_barrier();  // all reads of A and D done
       regs_to_lds(A, reg, nvec);
       regs_to_lds(D, dnext, nvec);
     }

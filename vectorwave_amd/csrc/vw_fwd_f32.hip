@@ -4,7 +4,13 @@
 
 namespace vw {
 
+// Unrolled tap counts; other L use the runtime-L kernels.  Dev builds may restrict the list:
+// make DEV_TAPS='X(8)' (the runtime-L kernel still covers every other L).
+#ifdef VW_DEV_TAPS
+#define VW_TAP_LIST(X) VW_DEV_TAPS(X)
+#else
 #define VW_TAP_LIST(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(24) X(30)
+#endif
 
 // Raise the dynamic-LDS limit once per kernel instantiation (a call per launch costs host time).
 // `configured` must be a static of the caller, which is unique per kernel instantiation.
@@ -19,9 +25,9 @@ static hipError_t set_lds(Kern k, int lds_bytes, int* configured) {
   return hipSuccess;
 }
 
-template <typename T, int L, bool FMA>
-static hipError_t run_forward_fused(const FwdArgs<T>& a, int threads, int lds, hipStream_t st) {
-  auto k = k_forward_fused<T, L, FMA>;
+template <typename T, int L, bool FMA, int NV>
+static hipError_t run_forward_fused_nv(const FwdArgs<T>& a, int threads, int lds, hipStream_t st) {
+  auto k = k_forward_fused<T, L, FMA, NV>;
   static int configured = 64 * 1024;
   hipError_t e = set_lds(k, lds, &configured);
   if (e != hipSuccess) return e;
@@ -29,16 +35,21 @@ static hipError_t run_forward_fused(const FwdArgs<T>& a, int threads, int lds, h
   return hipGetLastError();
 }
 
+template <typename T, int L, bool FMA>
+static hipError_t run_forward_fused(const FwdArgs<T>& a, int threads, int lds, int nv, hipStream_t st) {
+  return nv <= 4 ? run_forward_fused_nv<T, L, FMA, 4>(a, threads, lds, st) : run_forward_fused_nv<T, L, FMA, 8>(a, threads, lds, st);
+}
+
 template <typename T>
-hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds, bool fma, hipStream_t st) {
+hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds, bool fma, int nv, hipStream_t st) {
   switch (a.taps) {
 #define VW_CASE(n) \
-    case n: return fma ? run_forward_fused<T, n, true>(a, threads, lds, st) : run_forward_fused<T, n, false>(a, threads, lds, st);
+    case n: return fma ? run_forward_fused<T, n, true>(a, threads, lds, nv, st) : run_forward_fused<T, n, false>(a, threads, lds, nv, st);
     VW_TAP_LIST(VW_CASE)
 #undef VW_CASE
     default:
-      return fma ? run_forward_fused<T, 0, true>(a, threads, lds, st) : run_forward_fused<T, 0, false>(a, threads, lds, st);
+      return fma ? run_forward_fused<T, 0, true>(a, threads, lds, nv, st) : run_forward_fused<T, 0, false>(a, threads, lds, nv, st);
   }
 }
-template hipError_t launch_forward_fused<VW_T>(const FwdArgs<VW_T>&, int, int, bool, hipStream_t);
+template hipError_t launch_forward_fused<VW_T>(const FwdArgs<VW_T>&, int, int, bool, int, hipStream_t);
 }  // namespace vw

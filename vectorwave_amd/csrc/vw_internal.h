@@ -8,7 +8,7 @@ namespace vw {
 
 constexpr int kMaxTaps = 64;    // longest base filter accepted (COIF10 = 60 taps)
 constexpr int kMaxLevels = 24;  // batch semantics have no level cap; LDS / N bound it in practice
-constexpr int kNV = 8;          // vectors (16 B each) held per thread in the fused kernels
+constexpr int kNV = 8;          // max vectors (16 B each) held per thread in the fused kernels (NV = 4 or 8)
 constexpr int kMaxThreads = 1024;
 constexpr int kLdsBytes = 160 * 1024;
 
@@ -108,9 +108,9 @@ struct LevelArgs {
 
 // Launchers (vw_kernels.hip).  Return hipSuccess or the launch error.
 template <typename T>
-hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, hipStream_t st);
+hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
 template <typename T>
-hipError_t launch_inverse_fused(const InvArgs<T>& a, int threads, int lds_bytes, bool fma, hipStream_t st);
+hipError_t launch_inverse_fused(const InvArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
 template <typename T>
 hipError_t launch_forward_level(const LevelArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
 template <typename T>

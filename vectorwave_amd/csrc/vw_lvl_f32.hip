@@ -4,7 +4,13 @@
 
 namespace vw {
 
+// Unrolled tap counts; other L use the runtime-L kernels.  Dev builds may restrict the list:
+// make DEV_TAPS='X(8)' (the runtime-L kernel still covers every other L).
+#ifdef VW_DEV_TAPS
+#define VW_TAP_LIST(X) VW_DEV_TAPS(X)
+#else
 #define VW_TAP_LIST(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(24) X(30)
+#endif
 
 // Raise the dynamic-LDS limit once per kernel instantiation (a call per launch costs host time).
 // `configured` must be a static of the caller, which is unique per kernel instantiation.
