@@ -21,7 +21,8 @@ for s in $STEPS; do
       tail -3 gpurun_out/bench.log; echo "bench rc=$rc" ;;
     ab)  # quick variants: exact/fma, NV 4/8 (no CPU baseline)
       : > gpurun_out/ab.log
-      for v in "VW_NV=4" "VW_NV=8" "VW_NV=4 FMA=--fma" "VW_NV=8 FMA=--fma"; do
+      IFS=';' read -ra VARS <<< "${AB:-VW_NV=4;VW_NV=8;VW_NV=4 FMA=--fma;VW_NV=8 FMA=--fma}"
+      for v in "${VARS[@]}"; do
         env $v bash -c 'timeout -k 10 120 python bench.py --no-cpu-baseline --steps 30 $FMA' >> gpurun_out/ab.log 2>&1; rc=$?
         echo "$v rc=$rc" >> gpurun_out/ab.log
         fatal $rc && break

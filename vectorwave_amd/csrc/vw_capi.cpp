@@ -383,22 +383,52 @@ static vw_status report_bad(unsigned long long bad, int64_t N) {
 }
 
 // Plan of a fused launch: threads, vectors per thread (4 or 8), LDS bytes.  NV = 4 keeps the
-// per-thread register arrays small (no spills); NV = 8 reaches N = 1024 * 8 * V.
-static bool fused_plan(int64_t N, int V, int elem, int64_t lds_elems_extra, int* threads, int* nv, int* lds) {
+// per-thread register arrays small (no spills); NV = 8 reaches N = 1024 * 8 * V.  The workgroup is
+// ceil(nvec / NV) threads (not rounded to a wave): thread `tid` owns vectors tid + k*threads, and
+// the unrolled kernels rely on slabs 0..NV-2 being full, `fit` = (NV-1)*threads <= nvec (else the
+// runtime-L kernel with a bounds check per vector runs).
+static bool fused_plan(int64_t N, int V, int elem, int64_t lds_elems_extra, int* threads, int* nv, int* lds,
+                       bool* fit) {
   const int64_t nvec = (N + V - 1) / V;
   int want = 4;
   if (const char* e = getenv("VW_NV")) want = atoi(e) <= 4 ? 4 : 8;
-  if (round_up((nvec + want - 1) / want, 64) > kMaxThreads) want = 8;
-  int64_t th = round_up((nvec + want - 1) / want, 64);
-  th = std::max<int64_t>(th, 64);
-  if (const char* e = getenv("VW_MIN_THREADS")) th = std::max<int64_t>(th, atoi(e));
+  if ((nvec + want - 1) / want > kMaxThreads) want = 8;
+  const int64_t th = (nvec + want - 1) / want;
   if (th > kMaxThreads) return false;
-  *nv = want;
   const int64_t bytes = lds_elems_extra * elem;
   if (bytes > kLdsBytes) return false;
+  *nv = want;
   *threads = (int)th;
   *lds = (int)bytes;
+  *fit = (int64_t)(want - 1) * th <= nvec;
   return true;
+}
+
+// Owner-written halo of one level (vw_device.h halo_images): the affine images of an element and
+// the vector bands that have them; `own` only when every band lies in the slab that checks it.
+static void set_halo_images(LevelDesc& d, int64_t N, int64_t npow2, int V, int threads, int nv) {
+  int64_t s_el = 0, e_el = N;
+  d.il_a = 0; d.il_b = 1; d.ir_a = 0; d.ir_b = -1;  // no images
+  switch (d.mode) {
+    case kHaloPeriodic:
+      d.il_a = 1; d.il_b = (int)-N; d.ir_a = 1; d.ir_b = (int)N;
+      s_el = d.hr; e_el = N - d.hl;
+      break;
+    case kHaloSymmetric:
+      d.il_a = -1; d.il_b = -1; d.ir_a = -1; d.ir_b = (int)(2 * N - 1);
+      s_el = d.hl; e_el = N - d.hr;
+      break;
+    case kHaloFftPad:
+      d.il_a = 1; d.il_b = (int)-npow2;
+      e_el = npow2 - d.hl;
+      break;
+    default:
+      break;
+  }
+  e_el = std::min<int64_t>(std::max<int64_t>(e_el, 0), N);
+  d.vs = (int)((s_el + V - 1) / V);
+  d.ve = (int)(e_el / V);
+  d.own = (d.hl <= N && d.hr <= N && d.vs <= threads && (int64_t)d.ve >= (int64_t)(nv - 1) * threads) ? 1 : 0;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -440,13 +470,22 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
 
   const int hlpad = (int)round_up(max_hl, V);
   int threads = 0, lds = 0, nv = 4;
-  const int64_t lds_elems = hlpad + nvec * V + V;
-  if (J <= kMaxLevels && fused_plan(N, V, sizeof(T), lds_elems, &threads, &nv, &lds) && !getenv("VW_FORCE_TILED")) {
+  // Level buffers: two (one barrier per level) when they fit in LDS, else one.
+  const int64_t region = round_up(hlpad + nvec * V + V, V);
+  bool dbl = !getenv("VW_SINGLE_BUF");
+  bool fused = false, fit = false;
+  if (J <= kMaxLevels && !getenv("VW_FORCE_TILED")) {
+    if (dbl) dbl = fused_plan(N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
+    fused = dbl || fused_plan(N, V, sizeof(T), region, &threads, &nv, &lds, &fit);
+  }
+  if (fused) {
+    for (int j = 0; j < J; ++j) set_halo_images(lv[j], N, npow2, V, threads, nv);
     FwdArgs<T> a;
     memset(&a, 0, sizeof(a));
     a.x = x; a.ldx = ldx; a.details = details; a.approx = approx; a.B = B; a.N = (int)N; a.J = J;
-    a.npow2 = npow2; a.hlpad = hlpad;
+    a.npow2 = npow2; a.hlpad = hlpad; a.region1 = dbl ? (int)region : 0;
     a.vec_io = (ldx % V == 0) && (N % V == 0) && aligned16(x) && aligned16(details) && aligned16(approx);
+    a.unrolled = a.vec_io && fit;
     a.validate = validate; a.bad = c->bad;
     for (int j = 0; j < J; ++j) a.hist[j] = hist ? hist[j] : nullptr;
     a.hist_update = hist_update ? 1 : 0;
@@ -553,12 +592,26 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   const int hlpad = (int)round_up(max_hl, V);
   const int64_t region = round_up(hlpad + nvec * V + max_hr + V, V);
   int threads = 0, lds = 0, nv = 4;
-  if (fused_plan(N, V, sizeof(T), 2 * region, &threads, &nv, &lds) && !getenv("VW_FORCE_TILED")) {
+  // Pairwise sums need a_j and d_j together (two regions); sequential sums use two buffers when
+  // they fit (k_inverse_db, two barriers per level), else one time-shared region (k_inverse_seq).
+  bool db = !pair && !getenv("VW_SINGLE_BUF");
+  bool fused = false, fit = false;
+  if (!getenv("VW_FORCE_TILED")) {
+    if (pair || db) fused = fused_plan(N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
+    if (!fused && !pair) {
+      db = false;
+      fused = fused_plan(N, V, sizeof(T), region, &threads, &nv, &lds, &fit);
+    }
+  }
+  if (fused) {
+    for (int j = 0; j < J; ++j) set_halo_images(lv[j], N, 0, V, threads, nv);
     InvArgs<T> a;
     memset(&a, 0, sizeof(a));
     a.details = details; a.approx = approx; a.y = y; a.B = B; a.N = (int)N; a.J = J;
+    a.db = db ? 1 : 0;
     a.hlpad_a = hlpad; a.hlpad_d = hlpad; a.region_d = (int)region;
     a.vec_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
+    a.unrolled = a.vec_io && fit;
     a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.soft = soft; a.taps = L;
     copy_taps(a.lo, lo, L);
     copy_taps(a.hi, hi, L);

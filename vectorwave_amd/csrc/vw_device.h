@@ -69,6 +69,12 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// Wait for this wave's outstanding global loads (and stores) explicitly.  Used where every
+// outstanding op is one we need anyway: the waitcnt pass models exec-masked (skippable) blocks
+// conservatively, and without this it keeps the prologue loads "pending" into the level loop, where
+// it then waits for the detail stores of the previous level before touching those registers.
+__device__ __forceinline__ void wait_vmem() { __builtin_amdgcn_s_waitcnt(0x0F70); }  // vmcnt(0)
+
 // Value of a level input at signal index idx outside [0, N), read from the LDS copy `buf`
 // (element 0 at buf[0]).  The reference's index maps; see HaloMode.
 template <typename T>
@@ -280,28 +286,28 @@ __device__ __forceinline__ void inv_pair(const T* A, const T* D, int t0, int S, 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Global <-> LDS row transfers (16-byte vectors when aligned; scalar + zero tail otherwise).
-template <typename T>
-__device__ __forceinline__ void row_to_lds(T* buf, const T* __restrict__ src, int N, bool vec_ok,
-                                           int validate, unsigned long long* bad, unsigned long long flat0) {
-  constexpr int V = VT<T>::V;
-  using vec = typename VT<T>::v;
-  const int nvec = (N + V - 1) / V;
-  for (int w = threadIdx.x; w < nvec; w += blockDim.x) {
-    const int t0 = w * V;
-    vec v;
-    if (vec_ok && t0 + V <= N) {
-      v = __builtin_nontemporal_load(reinterpret_cast<const vec*>(src + t0));
-    } else {
+// Global <-> register <-> LDS row transfers.  A row is held as NV 16-byte vectors per lane, lane
+// `tid` owning vectors w = tid + k*NT (coalesced dwordx4 loads / stores, conflict-free b128 LDS).
+//
+// Scalar-instruction budget: the scalar unit is shared by the CU's four SIMDs, and per-vector
+// runtime checks (bounds, modes, spacing, direction) cost several SALU + a branch each.  So the
+// fused kernels make every such decision once per level (row functions below, templated on the
+// spacing class and direction), and only the last of a thread's NV vectors carries a bounds check:
+// the host sizes the workgroup so that slabs 0..NV-2 are full ((NV-1)*NT <= nvec, vw_capi.cpp).
+template <int L, int NV, typename F>
+__device__ __forceinline__ void for_vecs(int nvec, F&& fn) {
+  const int NT = blockDim.x;
 #pragma unroll
-      for (int e = 0; e < V; ++e) v[e] = (t0 + e < N) ? src[t0 + e] : T(0);
-    }
-    if (validate) {
-#pragma unroll
-      for (int e = 0; e < V; ++e)
-        if (t0 + e < N && !finite_t(v[e])) atomicMin(bad, flat0 + (unsigned long long)(t0 + e));
-    }
-    *reinterpret_cast<vec*>(buf + t0) = v;
+  for (int k = 0; k < NV; ++k) {
+    int w = threadIdx.x + k * NT;
+    // Launder w: the addresses derived from it are loop-invariant across the level loop, and
+    // hoisting all of them (every vector x every buffer x every spacing path) out of it exhausts
+    // the 128-VGPR budget and spills.  Recomputing them per level costs a few VALU.
+    asm volatile("" : "+v"(w));
+    if ((L > 0 && k < NV - 1) || w < nvec) fn(k, w);
+    // ... and keep the scheduler from issuing the LDS reads of every vector at once (NV x L
+    // b128 reads in flight = all the VGPRs); 4 waves per SIMD hide the per-vector read latency.
+    __builtin_amdgcn_sched_barrier(0);
   }
 }
 
@@ -331,82 +337,8 @@ __device__ __forceinline__ void check_out(int validate, unsigned long long* bad,
     if (t0 + e < N && !finite_t(v[e])) atomicMin(bad, (1ull << 62) | (flat0 + (unsigned long long)(t0 + e)));
 }
 
-// ---------------------------------------------------------------------------------------------
-// Fused multi-level forward: MultiLevelMODWTTransform.decompose (:243-251) / BatchSIMDMODWT
-// .batchMultiLevelMODWTSoA (:362-377) / VectorWaveSwtAdapter.decomposeSWT (:370-390) /
-// BatchStreamingMODWT.processMultiLevel (:130-158) for one signal per workgroup.
-template <typename T, int L, bool FMA, int NV>
-__global__ void __launch_bounds__(kMaxThreads) k_forward_fused(const FwdArgs<T> p) {
-  constexpr int V = VT<T>::V;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  T* buf = reinterpret_cast<T*>(smem) + p.hlpad;
-  const long long b = blockIdx.x;
-  const int N = p.N;
-  const int nvec = (N + V - 1) / V;
-  const int NT = blockDim.x;
-  const int tid = threadIdx.x;
-  const bool vec_ok = p.vec_io != 0;
-  const unsigned long long flat0 = (unsigned long long)b * (unsigned long long)N;
-
-  row_to_lds(buf, p.x + b * p.ldx, N, vec_ok, p.validate, p.bad, flat0);
-
-  T areg[NV][V];
-  for (int j = 1; j <= p.J; ++j) {
-    const LevelDesc lv = p.lv[j - 1];
-    const T* hist_b = (lv.mode == kHaloHistory) ? p.hist[j - 1] + b * lv.hist_len : nullptr;
-    lds_barrier();  // level input complete in LDS
-    fill_halo(buf, N, lv.hl, lv.hr, lv.mode, p.npow2, hist_b, lv.hist_len);
-    lds_barrier();  // halo complete
-
-    T* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
-    const bool last = (j == p.J);
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int w = tid + k * NT;
-      if (w < nvec) {
-        const int t0 = w * V;
-        T al[V], ah[V];
-#pragma unroll
-        for (int e = 0; e < V; ++e) { al[e] = T(0); ah[e] = T(0); }
-        fwd_vec<T, L, FMA>(buf, t0, lv.s, p.lo, p.hi, p.taps, al, ah);
-        store_vec(dout, t0, N, vec_ok, ah);
-        check_out<T>(p.validate, p.bad, flat0, t0, N, ah);
-        if (last) {
-          store_vec(p.approx + b * (size_t)N, t0, N, vec_ok, al);
-          check_out<T>(p.validate, p.bad, flat0, t0, N, al);
-        } else {
-          check_out<T>(p.validate, p.bad, flat0, t0, N, al);
-        }
-#pragma unroll
-        for (int e = 0; e < V; ++e) areg[k][e] = al[e];
-      }
-    }
-    // Streaming: new left history = last hist_len samples of this level's input
-    // (BatchStreamingMODWT.updateHistoryFromSoA :337-352; buf[<0] holds the old history).
-    if (p.hist_update && lv.hist_len > 0) {
-      T* hnew = p.hist[j - 1] + b * lv.hist_len;
-      for (int q = tid; q < lv.hist_len; q += NT) hnew[q] = buf[q + N - lv.hist_len];
-    }
-    if (!last) {
-      lds_barrier();  // every read of this level's input done
-#pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        const int w = tid + k * NT;
-        if (w < nvec) {
-          typename VT<T>::v o;
-#pragma unroll
-          for (int e = 0; e < V; ++e) o[e] = areg[k][e];
-          *reinterpret_cast<typename VT<T>::v*>(buf + w * V) = o;
-        }
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Fused multi-level inverse: MultiLevelMODWTTransform.reconstruct (:339-349, :554-645),
-// VectorWaveSwtAdapter.reconstructPeriodic (:444-474), MODWTTransform.inverse (J=1, pairwise),
-// with the denoise threshold (MutableMultiLevelMODWTResult.java:97-114) fused into the detail load.
+// MutableMultiLevelMODWTResult.applyThreshold (:97-114): soft = signum(c)*(|c|-T) above T, hard
+// keeps c when |c| > T.
 template <typename T>
 __device__ __forceinline__ T threshold_t(T c, T thr, int soft) {
   const T av = c < T(0) ? -c : c;
@@ -420,52 +352,316 @@ __device__ __forceinline__ T threshold_t(T c, T thr, int soft) {
   return av <= thr ? T(0) : c;
 }
 
+// Issue the loads of one row into registers.  Loads only: the values are first touched where they
+// are written to LDS (the zero / threshold selection is applied there), so a prefetch is never
+// waited for early.  The vector loads are unconditional (lanes past the row re-read its last vector;
+// those registers are never used): an exec-masked load in its own basic block makes the waitcnt
+// pass lose count and wait vmcnt(0) at the first use, i.e. for every load in flight.  The unrolled
+// kernels (L > 0) only run on 16-byte-aligned rows; the scalar form is the runtime-L kernel's.
 template <typename T, int NV>
 __device__ __forceinline__ void load_row_regs(T (&r)[NV][VT<T>::V], const T* __restrict__ src, int N, int nvec,
-                                              bool vec_ok, bool zero, const T* thr, T thr_b, int soft) {
+                                              bool vec_ok, bool zero) {
   constexpr int V = VT<T>::V;
   using vec = typename VT<T>::v;
   const int NT = blockDim.x;
+  if (zero) return;  // r stays undefined; the writer substitutes zeros
+  if (vec_ok) {
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int w = threadIdx.x + k * NT;
-    if (w < nvec) {
-      const int t0 = w * V;
-      if (zero) {
+    for (int k = 0; k < NV; ++k) {
+      int w = (int)threadIdx.x + k * NT;
+      asm volatile("" : "+v"(w));  // not hoisted out of the level loop (see for_vecs)
+      w = min(w, nvec - 1);
+      const vec v = __builtin_nontemporal_load(reinterpret_cast<const vec*>(src + w * V));
 #pragma unroll
-        for (int e = 0; e < V; ++e) r[k][e] = T(0);
-      } else if (vec_ok && t0 + V <= N) {
-        const vec v = __builtin_nontemporal_load(reinterpret_cast<const vec*>(src + t0));
+      for (int e = 0; e < V; ++e) r[k][e] = v[e];
+    }
+  } else {
 #pragma unroll
-        for (int e = 0; e < V; ++e) r[k][e] = v[e];
-      } else {
+    for (int k = 0; k < NV; ++k) {
+      const int w = threadIdx.x + k * NT;
+      if (w < nvec) {
+        const int t0 = w * V;
 #pragma unroll
         for (int e = 0; e < V; ++e) r[k][e] = (t0 + e < N) ? src[t0 + e] : T(0);
       }
-      if (thr) {
-#pragma unroll
-        for (int e = 0; e < V; ++e) r[k][e] = threshold_t(r[k][e], thr_b, soft);
-      }
     }
   }
+}
+
+// ---- Halo by owner writes ---------------------------------------------------------------------
+// Whoever writes element t of a level input into LDS also writes the halo positions the
+// reference's index map sends to t, so the halo costs no extra pass and no extra barrier.  With
+// hl <= N and hr <= N an element has at most one image per side, an affine function of t:
+//   periodic  (i mod N):             t - N (left), t + N (right)
+//   symmetric (MathUtils mirror):    -t - 1 (left), 2N - 1 - t (right)
+//   fftpad    (i + nextPow2(N) < N):  t - npow2 (left); right halo is zero
+// (LevelDesc il_*/ir_*; an image is written when it falls inside [-hl, 0) / [N, N+hr)).  Only
+// vectors w < vs (in the thread's first slab) or w >= ve (in its last slab) have images.
+// Positions with no source (zero padding, fftpad gaps, streaming history) are written by
+// halo_fixed.  When these conditions do not hold the host clears LevelDesc::own and the kernels
+// fill the halo from LDS after a barrier (fill_halo), as the reference's modulo does for any index.
+template <typename T>
+__device__ __forceinline__ void halo_images(T* buf, int w, const typename VT<T>::v& o, int N, const LevelDesc& lv) {
+  constexpr int V = VT<T>::V;
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    const int t = w * V + e;
+    if (t < N) {
+      const int l = lv.il_a * t + lv.il_b;
+      const int r = lv.ir_a * t + lv.ir_b;
+      if (l < 0 && l >= -lv.hl) buf[l] = o[e];
+      if (r >= N && r < N + lv.hr) buf[r] = o[e];
+    }
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void halo_fixed(T* buf, int N, const LevelDesc& lv, int npow2, const T* hist_b) {
+  if (lv.mode == kHaloPeriodic || lv.mode == kHaloSymmetric) return;
+  const int total = lv.hl + lv.hr;
+  for (int q = threadIdx.x; q < total; q += blockDim.x) {
+    const int idx = q < lv.hl ? q - lv.hl : N + (q - lv.hl);
+    if (lv.mode == kHaloFftPad && idx < 0 && idx + npow2 < N) continue;  // an element's image
+    T v = T(0);
+    if (lv.mode == kHaloHistory && idx < 0 && idx >= -lv.hist_len) v = hist_b[lv.hist_len + idx];
+    buf[idx] = v;
+  }
+}
+
+// Write a register-held row into the LDS level buffer `buf` with its halo for level `lv`.
+// MODE 0: values as is; 1: zeros (masked-out level, registers never loaded); 2: thresholded.
+template <typename T, int L, int NV, int MODE>
+__device__ __forceinline__ void regs_to_level_m(T* buf, const T (&r)[NV][VT<T>::V], int nvec, int N,
+                                                const LevelDesc& lv, T thr_b, int soft) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  const bool own = lv.own != 0;
+  for_vecs<L, NV>(nvec, [&](int k, int w) {
+    vec o;
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      if constexpr (MODE == 1) o[e] = T(0);
+      else if constexpr (MODE == 2) o[e] = threshold_t(r[k][e], thr_b, soft);
+      else o[e] = r[k][e];
+    }
+    if (L > 0 || w * V + V <= N) {
+      *reinterpret_cast<vec*>(buf + w * V) = o;
+    } else {  // ragged tail: positions >= N belong to the right halo (written by their owners)
+#pragma unroll
+      for (int e = 0; e < V; ++e)
+        if (w * V + e < N) buf[w * V + e] = o[e];
+    }
+    if (own && ((k == 0 && w < lv.vs) || (k == NV - 1 && w >= lv.ve))) halo_images(buf, w, o, N, lv);
+  });
+}
+
+// If the level cannot use owner writes this ends with a barrier and the generic halo fill; either
+// way the caller's next lds_barrier() publishes data + halo.
+template <typename T, int L, int NV>
+__device__ __forceinline__ void regs_to_level(T* buf, const T (&r)[NV][VT<T>::V], int nvec, int N, const LevelDesc& lv,
+                                              int npow2, const T* hist_b, bool zero = false, const T* thr = nullptr,
+                                              T thr_b = T(0), int soft = 0) {
+  if (zero) regs_to_level_m<T, L, NV, 1>(buf, r, nvec, N, lv, thr_b, soft);
+  else if (thr) regs_to_level_m<T, L, NV, 2>(buf, r, nvec, N, lv, thr_b, soft);
+  else regs_to_level_m<T, L, NV, 0>(buf, r, nvec, N, lv, thr_b, soft);
+  if (lv.own) {
+    halo_fixed(buf, N, lv, npow2, hist_b);
+  } else {
+    lds_barrier();
+    fill_halo(buf, N, lv.hl, lv.hr, lv.mode, npow2, hist_b, lv.hist_len);
+  }
+}
+
+// ---- Row compute: one level's convolution over the thread's NV vectors -------------------------
+// Forward, both filters from one set of LDS reads; emit(k, w, al, ah) consumes each output vector.
+// SC: 1 / 2 = register window for spacing 1 / 2 (the latter fp32 only), 0 = strided b128 reads.
+template <typename T, int L, bool FMA, int NV, int SC, typename Emit>
+__device__ __forceinline__ void fwd_row_t(const T* buf, int nvec, int s, const T* lo, const T* hi, int taps,
+                                          Emit&& emit) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  for_vecs<L, NV>(nvec, [&](int k, int w) {
+    const int t0 = w * V;
+    T al[V], ah[V];
+#pragma unroll
+    for (int e = 0; e < V; ++e) { al[e] = T(0); ah[e] = T(0); }
+    if constexpr (L > 0 && SC > 0) {
+      fwd_window<T, L, FMA, SC>(buf, t0, lo, hi, al, ah);
+    } else if constexpr (L > 0) {
+#pragma unroll
+      for (int i = 0; i < L; ++i) {  // s is a multiple of V: aligned 16-byte reads
+        const vec v = *reinterpret_cast<const vec*>(buf + t0 - i * s);
+#pragma unroll
+        for (int e = 0; e < V; ++e) {
+          al[e] = madd<FMA>(al[e], v[e], lo[i]);
+          ah[e] = madd<FMA>(ah[e], v[e], hi[i]);
+        }
+      }
+    } else {
+      fwd_vec<T, 0, FMA>(buf, t0, s, lo, hi, taps, al, ah);
+    }
+    emit(k, w, al, ah);
+  });
+}
+
+template <typename T, int L, bool FMA, int NV, typename Emit>
+__device__ __forceinline__ void fwd_row(const T* buf, int nvec, int s, const T* lo, const T* hi, int taps,
+                                        Emit&& emit) {
+  constexpr int V = VT<T>::V;
+  if constexpr (L > 0) {
+    if (s == 1) return fwd_row_t<T, L, FMA, NV, 1>(buf, nvec, s, lo, hi, taps, emit);
+    if constexpr (V == 4) {
+      if (s == 2) return fwd_row_t<T, L, FMA, NV, 2>(buf, nvec, s, lo, hi, taps, emit);
+    }
+  }
+  fwd_row_t<T, L, FMA, NV, 0>(buf, nvec, s, lo, hi, taps, emit);
+}
+
+// Inverse, one branch over the row: acc[k]_e (+)= f[i] * buf[t0 + e + dir*i*s + off], i ascending
+// (MultiLevelMODWTTransform.java:578-588 periodic, :612-639 symmetric orientations).
+// SC as above; SC = -1: generic per-element form (runtime taps, or an offset that is not a
+// multiple of V -- the symmetric alignment shifts).
+template <typename T, int L, bool FMA, int NV, int SC, int DIR>
+__device__ __forceinline__ void inv_row_t(const T* buf, int nvec, int s, int dir, int off, const T* f, int taps,
+                                          T (&acc)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  for_vecs<L, NV>(nvec, [&](int k, int w) {
+    const int t0 = w * V;
+    if constexpr (L > 0 && SC > 0) {
+      inv_window<T, L, FMA, SC, DIR>(buf, t0 + off, f, acc[k]);
+    } else if constexpr (L > 0 && SC == 0) {
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+        const vec v = *reinterpret_cast<const vec*>(buf + t0 + off + DIR * i * s);
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[k][e] = madd<FMA>(acc[k][e], v[e], f[i]);
+      }
+    } else {
+      inv_branch<T, L, FMA>(buf, t0, s, dir, off, f, taps, acc[k]);
+    }
+    // Pin the sums here: otherwise the arithmetic is sunk to the next use of acc (the other branch,
+    // after a barrier) while the LDS reads stay put, and every read value is live until then.
+#pragma unroll
+    for (int e = 0; e < V; ++e) asm volatile("" : "+v"(acc[k][e]));
+  });
+}
+
+template <typename T, int L, bool FMA, int NV>
+__device__ __forceinline__ void inv_row(const T* buf, int nvec, int s, int dir, int off, const T* f, int taps,
+                                        T (&acc)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  if constexpr (L > 0) {
+    if ((off & (V - 1)) == 0) {
+      if (s == 1) {
+        if (dir > 0) return inv_row_t<T, L, FMA, NV, 1, 1>(buf, nvec, s, dir, off, f, taps, acc);
+        return inv_row_t<T, L, FMA, NV, 1, -1>(buf, nvec, s, dir, off, f, taps, acc);
+      }
+      if constexpr (V == 4) {
+        if (s == 2) {
+          if (dir > 0) return inv_row_t<T, L, FMA, NV, 2, 1>(buf, nvec, s, dir, off, f, taps, acc);
+          return inv_row_t<T, L, FMA, NV, 2, -1>(buf, nvec, s, dir, off, f, taps, acc);
+        }
+      }
+      if (dir > 0) return inv_row_t<T, L, FMA, NV, 0, 1>(buf, nvec, s, dir, off, f, taps, acc);
+      return inv_row_t<T, L, FMA, NV, 0, -1>(buf, nvec, s, dir, off, f, taps, acc);
+    }
+  }
+  inv_row_t<T, L, FMA, NV, -1, 1>(buf, nvec, s, dir, off, f, taps, acc);
 }
 
 template <typename T, int NV>
-__device__ __forceinline__ void regs_to_lds(T* buf, const T (&r)[NV][VT<T>::V], int nvec) {
+__device__ __forceinline__ void zero_regs(T (&r)[NV][VT<T>::V]) {
+#pragma unroll
+  for (int k = 0; k < NV; ++k)
+#pragma unroll
+    for (int e = 0; e < VT<T>::V; ++e) r[k][e] = T(0);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fused multi-level forward: MultiLevelMODWTTransform.decompose (:243-251) / BatchSIMDMODWT
+// .batchMultiLevelMODWTSoA (:362-377) / VectorWaveSwtAdapter.decomposeSWT (:370-390) /
+// BatchStreamingMODWT.processMultiLevel (:130-158) for one signal per workgroup.
+//
+// Level inputs alternate between two LDS buffers (p.region1 != 0): level j reads X while its
+// approximation -- the input of level j+1, halo included -- is written into Y, so each level costs
+// ONE workgroup barrier.  With one buffer (long signals), a second barrier guards the overwrite.
+template <typename T, int L, bool FMA, int NV, bool VALIDATE>
+__device__ __forceinline__ void fwd_level(const FwdArgs<T>& p, const T* X, int nvec, const LevelDesc& lv, T* dout,
+                                          T* aout, bool vec_ok, unsigned long long flat0, T (&areg)[NV][VT<T>::V]) {
   constexpr int V = VT<T>::V;
+  const int N = p.N;
+  fwd_row<T, L, FMA, NV>(X, nvec, lv.s, p.lo, p.hi, p.taps, [&](int k, int w, const T (&al)[V], const T (&ah)[V]) {
+    const int t0 = w * V;
+    store_vec(dout, t0, N, vec_ok, ah);
+    if (aout) store_vec(aout, t0, N, vec_ok, al);
+    if constexpr (VALIDATE) {
+      check_out<T>(1, p.bad, flat0, t0, N, ah);
+      check_out<T>(1, p.bad, flat0, t0, N, al);
+    }
+#pragma unroll
+    for (int e = 0; e < V; ++e) areg[k][e] = al[e];
+  });
+}
+
+template <typename T, int L, bool FMA, int NV>
+__global__ void __launch_bounds__(kMaxThreads) k_forward_fused(const FwdArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* X = reinterpret_cast<T*>(smem) + p.hlpad;
+  T* Y = p.region1 ? reinterpret_cast<T*>(smem) + p.region1 + p.hlpad : X;
+  const bool dbl = p.region1 != 0;
+  const long long b = blockIdx.x;
+  const int N = p.N;
+  const int nvec = (N + V - 1) / V;
   const int NT = blockDim.x;
+  const int tid = threadIdx.x;
+  const bool vec_ok = (L > 0) || p.vec_io != 0;  // unrolled kernels run with aligned rows only
+  const unsigned long long flat0 = (unsigned long long)b * (unsigned long long)N;
+  auto hist_of = [&](int j) -> const T* {  // level j's streaming history row (or nullptr)
+    const LevelDesc& d = p.lv[j - 1];
+    return d.mode == kHaloHistory ? p.hist[j - 1] + b * d.hist_len : nullptr;
+  };
+
+  T areg[NV][V];
+  load_row_regs<T, NV>(areg, p.x + b * p.ldx, N, nvec, vec_ok, false);
+  wait_vmem();
+  if (p.validate) {
+    for_vecs<L, NV>(nvec, [&](int k, int w) {
 #pragma unroll
-  for (int k = 0; k < NV; ++k) {
-    const int w = threadIdx.x + k * NT;
-    if (w < nvec) {
-      typename VT<T>::v o;
-#pragma unroll
-      for (int e = 0; e < V; ++e) o[e] = r[k][e];
-      *reinterpret_cast<typename VT<T>::v*>(buf + w * V) = o;
+      for (int e = 0; e < V; ++e)
+        if (w * V + e < N && !finite_t(areg[k][e])) atomicMin(p.bad, flat0 + (unsigned long long)(w * V + e));
+    });
+  }
+  regs_to_level<T, L, NV>(X, areg, nvec, N, p.lv[0], p.npow2, hist_of(1));
+
+  for (int j = 1; j <= p.J; ++j) {
+    const LevelDesc lv = p.lv[j - 1];
+    lds_barrier();  // X = level input + halo; every read of Y (previous level) done
+    T* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
+    T* aout = (j == p.J) ? p.approx + b * (size_t)N : nullptr;
+    if (p.validate) fwd_level<T, L, FMA, NV, true>(p, X, nvec, lv, dout, aout, vec_ok, flat0, areg);
+    else fwd_level<T, L, FMA, NV, false>(p, X, nvec, lv, dout, aout, vec_ok, flat0, areg);
+    // Streaming: new left history = last hist_len samples of this level's input
+    // (BatchStreamingMODWT.updateHistoryFromSoA :337-352).
+    if (p.hist_update && lv.hist_len > 0) {
+      T* hnew = p.hist[j - 1] + b * lv.hist_len;
+      for (int q = tid; q < lv.hist_len; q += NT) hnew[q] = X[q + N - lv.hist_len];
+    }
+    if (j < p.J) {
+      if (!dbl) lds_barrier();  // one buffer: every read of this level's input done first
+      regs_to_level<T, L, NV>(Y, areg, nvec, N, p.lv[j], p.npow2, hist_of(j + 1));
+      T* t = X; X = Y; Y = t;
     }
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused multi-level inverse: MultiLevelMODWTTransform.reconstruct (:339-349, :554-645),
+// VectorWaveSwtAdapter.reconstructPeriodic (:444-474), MODWTTransform.inverse (J=1, pairwise),
+// with the denoise threshold (MutableMultiLevelMODWTResult.java:97-114) fused into the detail load.
+//
+// Pairwise form (sum += h*a + g*d per tap): a_j and d_j in two LDS regions.
 template <typename T, int L, bool FMA, int NV>
 __global__ void __launch_bounds__(kMaxThreads) k_inverse_fused(const InvArgs<T> p) {
   constexpr int V = VT<T>::V;
@@ -475,65 +671,132 @@ __global__ void __launch_bounds__(kMaxThreads) k_inverse_fused(const InvArgs<T> 
   const long long b = blockIdx.x;
   const int N = p.N;
   const int nvec = (N + V - 1) / V;
-  const int NT = blockDim.x;
-  const int tid = threadIdx.x;
-  const bool vec_ok = p.vec_io != 0;
+  const bool vec_ok = (L > 0) || p.vec_io != 0;
   const T thr_b = p.thr ? p.thr[b] : T(0);
   const size_t plane = (size_t)p.B * (size_t)N;
 
   T reg[NV][V];
+  T dnext[NV][V];
   // coarsest level: approximation -> A, d_J -> D
-  load_row_regs<T, NV>(reg, p.approx + b * (size_t)N, N, nvec, vec_ok, p.approx_zero != 0, nullptr, T(0), 0);
-  regs_to_lds(A, reg, nvec);
-  {
-    const LevelDesc lv = p.lv[p.J - 1];
-    load_row_regs<T, NV>(reg, p.details + (size_t)(p.J - 1) * plane + b * (size_t)N, N, nvec, vec_ok, lv.use_d == 0,
-                  p.thr, thr_b, p.soft);
-    regs_to_lds(D, reg, nvec);
-  }
+  load_row_regs<T, NV>(reg, p.approx + b * (size_t)N, N, nvec, vec_ok, p.approx_zero != 0);
+  load_row_regs<T, NV>(dnext, p.details + (size_t)(p.J - 1) * plane + b * (size_t)N, N, nvec, vec_ok,
+                       p.lv[p.J - 1].use_d == 0);
+  wait_vmem();
+  regs_to_level<T, L, NV>(A, reg, nvec, N, p.lv[p.J - 1], 0, (const T*)nullptr, p.approx_zero != 0);
+  regs_to_level<T, L, NV>(D, dnext, nvec, N, p.lv[p.J - 1], 0, (const T*)nullptr, p.lv[p.J - 1].use_d == 0, p.thr,
+                          thr_b, p.soft);
 
   for (int j = p.J; j >= 1; --j) {
     const LevelDesc lv = p.lv[j - 1];
-    lds_barrier();  // A (level-j approximation) and D (d_j) complete
-    fill_halo(A, N, lv.hl, lv.hr, lv.mode, 0, (const T*)nullptr, 0);
-    fill_halo(D, N, lv.hl, lv.hr, lv.mode, 0, (const T*)nullptr, 0);
-    lds_barrier();
-
-    // prefetch d_{j-1} while this level computes (async-stage split)
-    T dnext[NV][V];
-    if (j > 1) {
+    lds_barrier();  // A (level-j approximation) and D (d_j) complete, halos included
+    if (j > 1) {    // prefetch d_{j-1} while this level computes
+      load_row_regs<T, NV>(dnext, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, vec_ok,
+                           p.lv[j - 2].use_d == 0);
+    }
+    for_vecs<L, NV>(nvec, [&](int k, int w) {
+      T acc[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = T(0);
+      inv_pair<T, L, FMA>(A, D, w * V, lv.s, lv.dir_a, p.lo, p.hi, p.taps, acc);
+#pragma unroll
+      for (int e = 0; e < V; ++e) reg[k][e] = acc[e];
+    });
+    if (j == 1) {
+      for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec(p.y + b * (size_t)N, w * V, N, vec_ok, reg[k]); });
+    } else {
       const LevelDesc ln = p.lv[j - 2];
-      load_row_regs<T, NV>(dnext, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, vec_ok, ln.use_d == 0,
-                    p.thr, thr_b, p.soft);
-    }
-#pragma unroll
-    for (int k = 0; k < NV; ++k) {
-      const int w = tid + k * NT;
-      if (w < nvec) {
-        const int t0 = w * V;
-        T acc[V];
-#pragma unroll
-        for (int e = 0; e < V; ++e) acc[e] = T(0);
-        if (p.pair) {
-          inv_pair<T, L, FMA>(A, D, t0, lv.s, lv.dir_a, p.lo, p.hi, p.taps, acc);
-        } else {
-          inv_branch<T, L, FMA>(A, t0, lv.s, lv.dir_a, lv.off_a, p.lo, p.taps, acc);
-          inv_branch<T, L, FMA>(D, t0, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
-        }
-        if (j == 1) {
-          store_vec(p.y + b * (size_t)N, t0, N, vec_ok, acc);
-        } else {
-#pragma unroll
-          for (int e = 0; e < V; ++e) reg[k][e] = acc[e];
-        }
-      }
-    }
-    if (j > 1) {
       lds_barrier();  // all reads of A and D done
-      regs_to_lds(A, reg, nvec);
-      regs_to_lds(D, dnext, nvec);
+      regs_to_level<T, L, NV>(A, reg, nvec, N, ln, 0, (const T*)nullptr);
+      wait_vmem();  // the d_{j-1} prefetch
+      regs_to_level<T, L, NV>(D, dnext, nvec, N, ln, 0, (const T*)nullptr, ln.use_d == 0, p.thr, thr_b, p.soft);
     }
   }
+}
+
+// Sequential-sum form (PERIODIC K4 / SYMMETRIC K6: all approximation taps, then all detail taps,
+// into one accumulator), double-buffered: X holds a_j, Y holds d_j.  Per level:
+//   barrier -> stage d_j (prefetched last level) into Y, prefetch d_{j-1} -> approx branch on X
+//   -> barrier -> detail branch on Y -> a_{j-1} into X
+// i.e. two workgroup barriers per level, and d_{j-1}'s loads have a whole level to land.
+template <typename T, int L, bool FMA, int NV>
+__global__ void __launch_bounds__(kMaxThreads) k_inverse_db(const InvArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* const X = reinterpret_cast<T*>(smem) + p.hlpad_a;
+  T* const Y = reinterpret_cast<T*>(smem) + p.region_d + p.hlpad_d;
+  const long long b = blockIdx.x;
+  const int N = p.N;
+  const int nvec = (N + V - 1) / V;
+  const bool vec_ok = (L > 0) || p.vec_io != 0;
+  const T thr_b = p.thr ? p.thr[b] : T(0);
+  const size_t plane = (size_t)p.B * (size_t)N;
+
+  T acc[NV][V];
+  T dreg[NV][V];
+  load_row_regs<T, NV>(acc, p.approx + b * (size_t)N, N, nvec, vec_ok, p.approx_zero != 0);
+  load_row_regs<T, NV>(dreg, p.details + (size_t)(p.J - 1) * plane + b * (size_t)N, N, nvec, vec_ok,
+                       p.lv[p.J - 1].use_d == 0);
+  wait_vmem();
+  regs_to_level<T, L, NV>(X, acc, nvec, N, p.lv[p.J - 1], 0, (const T*)nullptr, p.approx_zero != 0);
+
+  for (int j = p.J; j >= 1; --j) {
+    const LevelDesc lv = p.lv[j - 1];
+    lds_barrier();  // X = a_j + halo; every read of Y (previous level) done
+    wait_vmem();    // the d_j prefetch (the only global ops in flight)
+    regs_to_level<T, L, NV>(Y, dreg, nvec, N, lv, 0, (const T*)nullptr, lv.use_d == 0, p.thr, thr_b, p.soft);
+    if (j > 1)
+      load_row_regs<T, NV>(dreg, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, vec_ok,
+                           p.lv[j - 2].use_d == 0);
+    zero_regs<T, NV>(acc);
+    inv_row<T, L, FMA, NV>(X, nvec, lv.s, lv.dir_a, lv.off_a, p.lo, p.taps, acc);
+    lds_barrier();  // Y = d_j + halo; every read of X done
+    inv_row<T, L, FMA, NV>(Y, nvec, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
+    if (j > 1) regs_to_level<T, L, NV>(X, acc, nvec, N, p.lv[j - 2], 0, (const T*)nullptr);
+  }
+  for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec(p.y + b * (size_t)N, w * V, N, vec_ok, acc[k]); });
+}
+
+// Single-buffer sequential-sum form for signals too long for two LDS buffers: ONE region is
+// time-shared (a_j -> approx branch -> d_j -> detail branch -> a_{j-1}); four barriers per level.
+template <typename T, int L, bool FMA, int NV>
+__global__ void __launch_bounds__(kMaxThreads) k_inverse_seq(const InvArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* R = reinterpret_cast<T*>(smem) + p.hlpad_a;
+  const long long b = blockIdx.x;
+  const int N = p.N;
+  const int nvec = (N + V - 1) / V;
+  const bool vec_ok = (L > 0) || p.vec_io != 0;
+  const T thr_b = p.thr ? p.thr[b] : T(0);
+  const size_t plane = (size_t)p.B * (size_t)N;
+
+  T acc[NV][V];
+  T dreg[NV][V];
+  load_row_regs<T, NV>(acc, p.approx + b * (size_t)N, N, nvec, vec_ok, p.approx_zero != 0);
+  load_row_regs<T, NV>(dreg, p.details + (size_t)(p.J - 1) * plane + b * (size_t)N, N, nvec, vec_ok,
+                       p.lv[p.J - 1].use_d == 0);
+  wait_vmem();
+  regs_to_level<T, L, NV>(R, acc, nvec, N, p.lv[p.J - 1], 0, (const T*)nullptr, p.approx_zero != 0);
+
+  for (int j = p.J; j >= 1; --j) {
+    const LevelDesc lv = p.lv[j - 1];
+    lds_barrier();  // R = a_j + halo
+    zero_regs<T, NV>(acc);
+    inv_row<T, L, FMA, NV>(R, nvec, lv.s, lv.dir_a, lv.off_a, p.lo, p.taps, acc);
+    lds_barrier();  // every approximation-branch read done
+    wait_vmem();    // the d_j prefetch
+    regs_to_level<T, L, NV>(R, dreg, nvec, N, lv, 0, (const T*)nullptr, lv.use_d == 0, p.thr, thr_b, p.soft);
+    if (j > 1)
+      load_row_regs<T, NV>(dreg, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, vec_ok,
+                           p.lv[j - 2].use_d == 0);
+    lds_barrier();  // R = d_j + halo
+    inv_row<T, L, FMA, NV>(R, nvec, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
+    if (j > 1) {
+      lds_barrier();  // every detail-branch read done
+      regs_to_level<T, L, NV>(R, acc, nvec, N, p.lv[j - 2], 0, (const T*)nullptr);
+    }
+  }
+  for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec(p.y + b * (size_t)N, w * V, N, vec_ok, acc[k]); });
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -42,7 +42,7 @@ static hipError_t run_forward_fused(const FwdArgs<T>& a, int threads, int lds, i
 
 template <typename T>
 hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds, bool fma, int nv, hipStream_t st) {
-  switch (a.taps) {
+  switch (a.unrolled ? a.taps : 0) {  // unaligned rows / partial slabs: runtime-L kernel
 #define VW_CASE(n) \
     case n: return fma ? run_forward_fused<T, n, true>(a, threads, lds, nv, st) : run_forward_fused<T, n, false>(a, threads, lds, nv, st);
     VW_TAP_LIST(VW_CASE)

@@ -32,6 +32,10 @@ struct LevelDesc {
   int off_d;
   int use_d;    // inverse: 1 = d_j from memory, 0 = zero details (reconstructFromLevel / Levels)
   int hist_len; // streaming: left history length of this level (L_j - 1)
+  int own;      // 1: halo written by the element owners (vw_device.h halo_images), else filled after a barrier
+  int il_a, il_b;  // left image of element t: il_a*t + il_b (kept when in [-hl, 0))
+  int ir_a, ir_b;  // right image: ir_a*t + ir_b (kept when in [N, N+hr))
+  int vs, ve;   // only vectors w < vs or w >= ve have images
 };
 
 template <typename T>
@@ -45,7 +49,9 @@ struct FwdArgs {
   int J;
   int npow2;            // nextPow2(N) for kHaloFftPad
   int hlpad;            // LDS offset of element 0 (multiple of the vector width)
-  int vec_io;           // 1: rows and outputs are 16-B aligned -> vector global I/O
+  int region1;          // element offset of the second level buffer (0 = single buffer)
+  int vec_io;
+  int unrolled;         // 1: the tap-unrolled kernel may run (aligned rows, full slabs; vw_capi fused_plan)           // 1: rows and outputs are 16-B aligned -> vector global I/O
   int validate;         // 1: non-finite check on input and outputs (atomicMin into *bad)
   unsigned long long* bad;
   // streaming history (kHaloHistory): hist[j] is [B][hist_len_j], oldest first
@@ -69,6 +75,8 @@ struct InvArgs {
   int region_d;         // element offset of the D region start in LDS
   int vec_io;
   int pair;             // 1: sum += (h*a + g*d) per tap (MODWTTransform.inverse, ZERO multi-level)
+  int unrolled;
+  int db;               // sequential sum: 1 = two LDS buffers (k_inverse_db), 0 = one (k_inverse_seq)
   int approx_zero;
   const T* thr;         // per-signal threshold [B] (nullptr = no thresholding)
   int soft;

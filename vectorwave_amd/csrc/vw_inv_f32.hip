@@ -27,9 +27,10 @@ static hipError_t set_lds(Kern k, int lds_bytes, int* configured) {
 
 template <typename T, int L, bool FMA, int NV>
 static hipError_t run_inverse_fused_nv(const InvArgs<T>& a, int threads, int lds, hipStream_t st) {
-  auto k = k_inverse_fused<T, L, FMA, NV>;
-  static int configured = 64 * 1024;
-  hipError_t e = set_lds(k, lds, &configured);
+  // pairwise sums: k_inverse_fused; sequential sums: two LDS buffers (k_inverse_db) or one (k_inverse_seq)
+  static int configured_pair = 64 * 1024, configured_seq = 64 * 1024, configured_db = 64 * 1024;
+  auto k = a.pair ? k_inverse_fused<T, L, FMA, NV> : a.db ? k_inverse_db<T, L, FMA, NV> : k_inverse_seq<T, L, FMA, NV>;
+  hipError_t e = set_lds(k, lds, a.pair ? &configured_pair : a.db ? &configured_db : &configured_seq);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(threads), lds, st, a);
   return hipGetLastError();
@@ -42,7 +43,7 @@ static hipError_t run_inverse_fused(const InvArgs<T>& a, int threads, int lds, i
 
 template <typename T>
 hipError_t launch_inverse_fused(const InvArgs<T>& a, int threads, int lds, bool fma, int nv, hipStream_t st) {
-  switch (a.taps) {
+  switch (a.unrolled ? a.taps : 0) {  // unaligned rows / partial slabs: runtime-L kernel
 #define VW_CASE(n) \
     case n: return fma ? run_inverse_fused<T, n, true>(a, threads, lds, nv, st) : run_inverse_fused<T, n, false>(a, threads, lds, nv, st);
     VW_TAP_LIST(VW_CASE)
