@@ -392,7 +392,7 @@ static bool fused_plan(int64_t N, int V, int elem, int64_t lds_elems_extra, int*
   const int64_t nvec = (N + V - 1) / V;
   int want = 4;
   if (const char* e = getenv("VW_NV")) want = atoi(e) <= 4 ? 4 : 8;
-  if ((nvec + want - 1) / want > kMaxThreads) want = 8;
+  if ((nvec + want - 1) / want > 512) want = 8;  // NV = 4 kernels are bounded to 512 threads (VW_FUSED_BOUNDS)
   const int64_t th = (nvec + want - 1) / want;
   if (th > kMaxThreads) return false;
   const int64_t bytes = lds_elems_extra * elem;
@@ -470,9 +470,13 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
 
   const int hlpad = (int)round_up(max_hl, V);
   int threads = 0, lds = 0, nv = 4;
-  // Level buffers: two (one barrier per level) when they fit in LDS, else one.
+  // Level buffers: two (one barrier per level) or one (two barriers per level, but half the LDS:
+  // twice the workgroups per CU).  Measured on MI355X (db4 J=6, 4096 x 4096 fp64): the exact kernel
+  // is faster with one buffer (more workgroups to overlap its longer arithmetic), the FMA kernel
+  // with two.  VW_FWD_BUF=1|2 overrides.
   const int64_t region = round_up(hlpad + nvec * V + V, V);
-  bool dbl = !getenv("VW_SINGLE_BUF");
+  bool dbl = fma;
+  if (const char* e = getenv("VW_FWD_BUF")) dbl = atoi(e) == 2;
   bool fused = false, fit = false;
   if (J <= kMaxLevels && !getenv("VW_FORCE_TILED")) {
     if (dbl) dbl = fused_plan(N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
@@ -592,9 +596,12 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   const int hlpad = (int)round_up(max_hl, V);
   const int64_t region = round_up(hlpad + nvec * V + max_hr + V, V);
   int threads = 0, lds = 0, nv = 4;
-  // Pairwise sums need a_j and d_j together (two regions); sequential sums use two buffers when
-  // they fit (k_inverse_db, two barriers per level), else one time-shared region (k_inverse_seq).
-  bool db = !pair && !getenv("VW_SINGLE_BUF");
+  // Pairwise sums need a_j and d_j together (two regions).  Sequential sums time-share one region
+  // (k_inverse_seq, four barriers per level) -- measured faster on MI355X than two buffers
+  // (k_inverse_db, two barriers per level) because twice the workgroups fit per CU; VW_INV_BUF=2
+  // selects the latter.
+  bool db = false;
+  if (const char* e = getenv("VW_INV_BUF")) db = !pair && atoi(e) == 2;
   bool fused = false, fit = false;
   if (!getenv("VW_FORCE_TILED")) {
     if (pair || db) fused = fused_plan(N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);

@@ -263,6 +263,7 @@ __device__ __forceinline__ void inv_pair(const T* A, const T* D, int t0, int S, 
         const vec vd = *reinterpret_cast<const vec*>(D + t0 + i * step);
 #pragma unroll
         for (int e = 0; e < V; ++e) acc[e] = acc[e] + pair_term<T, FMA>(h[i], va[e], g[i], vd[e]);
+        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // <= 8 reads in flight (VGPR budget)
       }
       return;
     }
@@ -273,6 +274,7 @@ __device__ __forceinline__ void inv_pair(const T* A, const T* D, int t0, int S, 
         const int idx = t0 + e + dir * i * S;
         acc[e] = acc[e] + pair_term<T, FMA>(h[i], A[idx], g[i], D[idx]);
       }
+      if ((i & 1) == 1) __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight (VGPR budget)
     }
   } else {
     for (int i = 0; i < taps; ++i) {
@@ -343,10 +345,8 @@ template <typename T>
 __device__ __forceinline__ T threshold_t(T c, T thr, int soft) {
   const T av = c < T(0) ? -c : c;
   if (soft) {
-    if (av > thr) {
-      const T sg = c > T(0) ? T(1) : (c < T(0) ? T(-1) : c);  // Math.signum
-      return sg * (av - thr);
-    }
+    // Math.signum(c) * (|c| - T): c != 0 here, and a product with +-1 is a sign flip, i.e. copysign
+    if (av > thr) return __builtin_copysign(av - thr, c);
     return T(0);
   }
   return av <= thr ? T(0) : c;
@@ -440,7 +440,11 @@ __device__ __forceinline__ void regs_to_level_m(T* buf, const T (&r)[NV][VT<T>::
     vec o;
 #pragma unroll
     for (int e = 0; e < V; ++e) {
-      if constexpr (MODE == 1) o[e] = T(0);
+      if constexpr (MODE == 1) {
+        T z = T(0);
+        asm volatile("" : "+v"(z));  // materialised here, not a loop-invariant vector held in VGPRs
+        o[e] = z;
+      }
       else if constexpr (MODE == 2) o[e] = threshold_t(r[k][e], thr_b, soft);
       else o[e] = r[k][e];
     }
@@ -496,6 +500,7 @@ __device__ __forceinline__ void fwd_row_t(const T* buf, int nvec, int s, const T
           al[e] = madd<FMA>(al[e], v[e], lo[i]);
           ah[e] = madd<FMA>(ah[e], v[e], hi[i]);
         }
+        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // <= 4 reads in flight (VGPR budget)
       }
     } else {
       fwd_vec<T, 0, FMA>(buf, t0, s, lo, hi, taps, al, ah);
@@ -536,6 +541,7 @@ __device__ __forceinline__ void inv_row_t(const T* buf, int nvec, int s, int dir
         const vec v = *reinterpret_cast<const vec*>(buf + t0 + off + DIR * i * s);
 #pragma unroll
         for (int e = 0; e < V; ++e) acc[k][e] = madd<FMA>(acc[k][e], v[e], f[i]);
+        if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // <= 4 reads in flight (VGPR budget)
       }
     } else {
       inv_branch<T, L, FMA>(buf, t0, s, dir, off, f, taps, acc[k]);
@@ -578,6 +584,14 @@ __device__ __forceinline__ void zero_regs(T (&r)[NV][VT<T>::V]) {
     for (int e = 0; e < VT<T>::V; ++e) r[k][e] = T(0);
 }
 
+// Launch bounds of the fused kernels.  NV = 4: at most 512 threads and W waves per SIMD -- W = 8
+// (64 VGPRs: four 512-thread workgroups per CU, LDS permitting) for the forward, W = 6 (80 VGPRs,
+// three workgroups) for the inverse, whose prefetched detail row occupies 16 more VGPRs -- so
+// several workgroups share a CU and hide each other's barriers and row loads.  NV = 8 (long
+// signals): up to 1024 threads, 128 VGPRs.
+#define VW_FUSED_BOUNDS(NV, W) \
+  __attribute__((amdgpu_flat_work_group_size(1, (NV) <= 4 ? 512 : 1024), amdgpu_waves_per_eu((NV) <= 4 ? (W) : 4)))
+
 // ---------------------------------------------------------------------------------------------
 // Fused multi-level forward: MultiLevelMODWTTransform.decompose (:243-251) / BatchSIMDMODWT
 // .batchMultiLevelMODWTSoA (:362-377) / VectorWaveSwtAdapter.decomposeSWT (:370-390) /
@@ -605,7 +619,7 @@ __device__ __forceinline__ void fwd_level(const FwdArgs<T>& p, const T* X, int n
 }
 
 template <typename T, int L, bool FMA, int NV>
-__global__ void __launch_bounds__(kMaxThreads) k_forward_fused(const FwdArgs<T> p) {
+__global__ void VW_FUSED_BOUNDS(NV, 8) k_forward_fused(const FwdArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* X = reinterpret_cast<T*>(smem) + p.hlpad;
@@ -663,7 +677,7 @@ __global__ void __launch_bounds__(kMaxThreads) k_forward_fused(const FwdArgs<T> 
 //
 // Pairwise form (sum += h*a + g*d per tap): a_j and d_j in two LDS regions.
 template <typename T, int L, bool FMA, int NV>
-__global__ void __launch_bounds__(kMaxThreads) k_inverse_fused(const InvArgs<T> p) {
+__global__ void VW_FUSED_BOUNDS(NV, 6) k_inverse_fused(const InvArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* A = reinterpret_cast<T*>(smem) + p.hlpad_a;
@@ -699,7 +713,10 @@ __global__ void __launch_bounds__(kMaxThreads) k_inverse_fused(const InvArgs<T> 
       for (int e = 0; e < V; ++e) acc[e] = T(0);
       inv_pair<T, L, FMA>(A, D, w * V, lv.s, lv.dir_a, p.lo, p.hi, p.taps, acc);
 #pragma unroll
-      for (int e = 0; e < V; ++e) reg[k][e] = acc[e];
+      for (int e = 0; e < V; ++e) {
+        asm volatile("" : "+v"(acc[e]));  // pin the sum here (see inv_row_t)
+        reg[k][e] = acc[e];
+      }
     });
     if (j == 1) {
       for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec(p.y + b * (size_t)N, w * V, N, vec_ok, reg[k]); });
@@ -719,7 +736,7 @@ __global__ void __launch_bounds__(kMaxThreads) k_inverse_fused(const InvArgs<T> 
 //   -> barrier -> detail branch on Y -> a_{j-1} into X
 // i.e. two workgroup barriers per level, and d_{j-1}'s loads have a whole level to land.
 template <typename T, int L, bool FMA, int NV>
-__global__ void __launch_bounds__(kMaxThreads) k_inverse_db(const InvArgs<T> p) {
+__global__ void VW_FUSED_BOUNDS(NV, 6) k_inverse_db(const InvArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* const X = reinterpret_cast<T*>(smem) + p.hlpad_a;
@@ -759,7 +776,7 @@ __global__ void __launch_bounds__(kMaxThreads) k_inverse_db(const InvArgs<T> p) 
 // Single-buffer sequential-sum form for signals too long for two LDS buffers: ONE region is
 // time-shared (a_j -> approx branch -> d_j -> detail branch -> a_{j-1}); four barriers per level.
 template <typename T, int L, bool FMA, int NV>
-__global__ void __launch_bounds__(kMaxThreads) k_inverse_seq(const InvArgs<T> p) {
+__global__ void VW_FUSED_BOUNDS(NV, 6) k_inverse_seq(const InvArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* R = reinterpret_cast<T*>(smem) + p.hlpad_a;
