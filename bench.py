@@ -24,6 +24,10 @@ from ctypes import c_void_p
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+ACC_NAME = {
+    True: "fma (fused multiply-add per tap; max-abs error vs vectorwave-core < 1e-12, tests/test_gpu_parity.py)",
+    False: "exact (separate multiply and add in the reference's tap order; bit-identical to vectorwave-core)",
+}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
 
 CONFIGS = {
@@ -38,11 +42,14 @@ CONFIGS = {
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=200)   # ~0.1 s timed: long enough for stable clocks
+    p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--config", default="db4", choices=sorted(CONFIGS))
     p.add_argument("--batch", type=int, default=0, help="override signals per GPU")
-    p.add_argument("--fma", action="store_true", help="FMA accumulation (<=1e-12 vs the reference) instead of EXACT")
+    p.add_argument("--exact", action="store_true",
+                   help="headline in EXACT accumulation (bit-identical to vectorwave-core) instead of FMA")
+    p.add_argument("--fma", action="store_true", help="(default) FMA accumulation, max-abs error < 1e-12")
+    p.add_argument("--no-alt", action="store_true", help="skip the timing of the other accumulation mode")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU baseline sample")
     return p.parse_args()
@@ -78,14 +85,17 @@ def main():
     esz = 4 if dtype == "f32" else 8
     dev = torch.device("cuda", local)
 
-    # rank r owns global signals [r*Bg, (r+1)*Bg): distinct data per rank, no exchange
+    # weak scaling: the global batch is world*Bg signals; rank r owns its shard_rows() block
+    # (distinct data per rank, generated on device from the global row index), no exchange
+    from vectorwave_amd.shard import shard_rows
+    start, Bg = shard_rows(world * Bg, world, rank)
     x = torch.empty((Bg, N), dtype=tdt, device=dev)
-    eng.fill_uniform(x, 42, offset=rank * Bg * N)
+    eng.fill_uniform(x, 42, offset=start * N)
     det = torch.empty((J, Bg, N), dtype=tdt, device=dev)
     app = torch.empty((Bg, N), dtype=tdt, device=dev)
     y = torch.empty((Bg, N), dtype=tdt, device=dev)
     eng.bind_torch_stream()
-    flags = nat.FLAG_FMA if args.fma else 0
+    flags = 0 if args.exact else nat.FLAG_FMA
     lo_a, hi_a = nat.taps_array(lo), nat.taps_array(hi)
     fwd = lib.vw_modwt_forward_f32 if dtype == "f32" else lib.vw_modwt_forward_f64
     inv = lib.vw_modwt_inverse_f32 if dtype == "f32" else lib.vw_modwt_inverse_f64
@@ -96,7 +106,7 @@ def main():
             raise RuntimeError(f"engine status {st}: {nat.last_error()}")
 
     if pipeline == "fwd+inv":
-        def step():
+        def step(flags=flags):
             check(fwd(eng.ctx, xp, Bg, N, N, lo_a, hi_a, L, w.wavelet_id, nat.PERIODIC, J, flags, dp, ap))
             check(inv(eng.ctx, dp, ap, Bg, N, lo_a, hi_a, L, w.wavelet_id, nat.PERIODIC, J, 0xFFFFFFFF, 0, flags, yp))
         bytes_per_sample = {"forward": (J + 2) * esz, "inverse": (J + 2) * esz}
@@ -104,7 +114,7 @@ def main():
         thr = torch.empty((Bg,), dtype=torch.float64, device=dev)
         tp = c_void_p(thr.data_ptr())
 
-        def step():
+        def step(flags=flags):
             check(lib.vw_swt_denoise_f64(eng.ctx, xp, Bg, N, N, lo_a, hi_a, L, w.wavelet_id, nat.PERIODIC, J, -1.0, 1,
                                          flags, yp, tp))
         bytes_per_sample = {"forward": (J + 2) * esz, "inverse": (J + 2) * esz, "sigma": esz}
@@ -160,6 +170,38 @@ def main():
         except Exception:
             traffic = None
 
+    # The other accumulation mode, same workload, timed the same way (reported beside the headline).
+    alt = None
+    if not args.no_alt:
+        aflags = flags ^ nat.FLAG_FMA
+        for _ in range(args.warmup):
+            step(aflags)
+        eng.reset_timing()
+        eng.enable_timing(True)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        a0 = time.perf_counter()
+        for _ in range(args.steps):
+            step(aflags)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        a1 = time.perf_counter()
+        eng.enable_timing(False)
+        aelapsed = a1 - a0
+        if world > 1:
+            tt = torch.tensor([aelapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            aelapsed = tt.item()
+        akern = {}
+        for k in ("forward", "inverse", "sigma", "forward_level", "inverse_level"):
+            ms, n = eng.kernel_time(k)
+            if n:
+                akern[k] = round(ms / n, 5)
+        alt = {"accumulation": ACC_NAME[bool(aflags & nat.FLAG_FMA)],
+               "value": round(units * world * args.steps / aelapsed / 1e6, 2), "kernels_ms": akern}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(w, J, N, dtype, pipeline, args.cpu_seconds)
@@ -182,9 +224,10 @@ def main():
             "config": {
                 "workload": f"{wname} MODWT J={J} {pipeline}, {Bg} signals x {N} samples per GPU, {dtype}, PERIODIC",
                 "wavelet": wname, "levels": J, "batch_per_gpu": Bg, "signal_length": N, "boundary": "PERIODIC",
-                "accumulation": "fma" if args.fma else "exact (bit-identical to vectorwave-core)",
+                "accumulation": ACC_NAME[bool(flags & nat.FLAG_FMA)],
                 "parallelism": f"batch-shard x{world} (no collective)",
                 "kernels_ms": {k: round(v[0], 5) for k, v in fam.items()},
+                "other_accumulation": alt,
             },
             "roofline": {
                 "bound": "hbm", "kernel": dom, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -19,11 +19,11 @@ for s in $STEPS; do
     bench)
       timeout -k 10 300 python bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1; rc=$?
       tail -3 gpurun_out/bench.log; echo "bench rc=$rc" ;;
-    ab)  # quick variants: exact/fma, NV 4/8 (no CPU baseline)
+    ab)  # quick env variants (no CPU baseline, headline mode only; FMA=--exact selects exact accumulation)
       : > gpurun_out/ab.log
-      IFS=';' read -ra VARS <<< "${AB:-VW_NV=4;VW_NV=8;VW_NV=4 FMA=--fma;VW_NV=8 FMA=--fma}"
+      IFS=';' read -ra VARS <<< "${AB:-X=1;FMA=--exact}"
       for v in "${VARS[@]}"; do
-        env $v bash -c 'timeout -k 10 120 python bench.py --no-cpu-baseline --steps 30 $FMA' >> gpurun_out/ab.log 2>&1; rc=$?
+        env $v bash -c 'timeout -k 10 120 python bench.py --no-cpu-baseline --no-alt --steps 30 $FMA' >> gpurun_out/ab.log 2>&1; rc=$?
         echo "$v rc=$rc" >> gpurun_out/ab.log
         fatal $rc && break
       done
@@ -31,6 +31,16 @@ for s in $STEPS; do
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1; rc=$?
       tail -3 gpurun_out/prof.log; echo "prof rc=$rc" ;;
+    traffic)  # HBM bytes per launch (PMC FETCH_SIZE / WRITE_SIZE, separate passes) -> gpurun_out/hbm_traffic_<cfg>.json
+      rm -rf gpurun_out/pmc
+      PMC_GROUPS="FETCH_SIZE
+WRITE_SIZE" BENCH_ARGS="${BENCH_ARGS:-}" bash tools/pmc.sh; rc=$?
+      if [ $rc -eq 0 ]; then
+        python3 tools/hbm_traffic.py gpurun_out/pmc > gpurun_out/hbm_traffic_${CFG:-db4}.json
+        python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc_traffic_${CFG:-db4}.txt
+        cat gpurun_out/hbm_traffic_${CFG:-db4}.json
+      fi
+      echo "traffic rc=$rc" ;;
     *) echo "unknown step $s"; rc=0 ;;
   esac
   if fatal $rc; then echo "fatal rc=$rc at step $s, stopping"; exit $rc; fi

@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
-ARGS="${BENCH_ARGS:-} --no-cpu-baseline --steps 3 --warmup 1"
+ARGS="${BENCH_ARGS:-} --no-cpu-baseline --no-alt --steps 3 --warmup 1"
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
