@@ -46,6 +46,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=50)
     p.add_argument("--config", default="db4", choices=sorted(CONFIGS))
     p.add_argument("--batch", type=int, default=0, help="override signals per GPU")
+    p.add_argument("--wavelet", default="", help="override the config's wavelet (experiments)")
     p.add_argument("--exact", action="store_true",
                    help="headline in EXACT accumulation (bit-identical to vectorwave-core) instead of FMA")
     p.add_argument("--fma", action="store_true", help="(default) FMA accumulation, max-abs error < 1e-12")
@@ -76,6 +77,8 @@ def main():
     wname, J, Bg, N, dtype, pipeline = CONFIGS[args.config]
     if args.batch:
         Bg = args.batch
+    if args.wavelet:
+        wname = args.wavelet
     w = vw.get_wavelet(wname)
     lo, hi = w.lowPassDecomposition(), w.highPassDecomposition()
     L = len(lo)

@@ -23,7 +23,7 @@ for s in $STEPS; do
       : > gpurun_out/ab.log
       IFS=';' read -ra VARS <<< "${AB:-X=1;FMA=--exact}"
       for v in "${VARS[@]}"; do
-        env $v bash -c 'timeout -k 10 120 python bench.py --no-cpu-baseline --no-alt --steps 30 $FMA' >> gpurun_out/ab.log 2>&1; rc=$?
+        env $v bash -c 'timeout -k 10 120 python bench.py --no-cpu-baseline --no-alt --steps 300 $FMA' >> gpurun_out/ab.log 2>&1; rc=$?
         echo "$v rc=$rc" >> gpurun_out/ab.log
         fatal $rc && break
       done

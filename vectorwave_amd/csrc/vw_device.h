@@ -589,6 +589,9 @@ __device__ __forceinline__ void zero_regs(T (&r)[NV][VT<T>::V]) {
 // three workgroups) for the inverse, whose prefetched detail row occupies 16 more VGPRs -- so
 // several workgroups share a CU and hide each other's barriers and row loads.  NV = 8 (long
 // signals): up to 1024 threads, 128 VGPRs.
+// Longer filters need wider register windows (the s = 1 window holds L + V - 1 values): L <= 8 gets
+// W waves, longer filters 4 (128 VGPRs; with 512-thread workgroups 5 waves would not add one).
+#define VW_FUSED_W(L, W) ((L) <= 8 ? (W) : 4)
 #define VW_FUSED_BOUNDS(NV, W) \
   __attribute__((amdgpu_flat_work_group_size(1, (NV) <= 4 ? 512 : 1024), amdgpu_waves_per_eu((NV) <= 4 ? (W) : 4)))
 
@@ -619,7 +622,7 @@ __device__ __forceinline__ void fwd_level(const FwdArgs<T>& p, const T* X, int n
 }
 
 template <typename T, int L, bool FMA, int NV>
-__global__ void VW_FUSED_BOUNDS(NV, 8) k_forward_fused(const FwdArgs<T> p) {
+__global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_fused(const FwdArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* X = reinterpret_cast<T*>(smem) + p.hlpad;
@@ -677,7 +680,7 @@ __global__ void VW_FUSED_BOUNDS(NV, 8) k_forward_fused(const FwdArgs<T> p) {
 //
 // Pairwise form (sum += h*a + g*d per tap): a_j and d_j in two LDS regions.
 template <typename T, int L, bool FMA, int NV>
-__global__ void VW_FUSED_BOUNDS(NV, 6) k_inverse_fused(const InvArgs<T> p) {
+__global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_fused(const InvArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* A = reinterpret_cast<T*>(smem) + p.hlpad_a;
@@ -736,7 +739,7 @@ __global__ void VW_FUSED_BOUNDS(NV, 6) k_inverse_fused(const InvArgs<T> p) {
 //   -> barrier -> detail branch on Y -> a_{j-1} into X
 // i.e. two workgroup barriers per level, and d_{j-1}'s loads have a whole level to land.
 template <typename T, int L, bool FMA, int NV>
-__global__ void VW_FUSED_BOUNDS(NV, 6) k_inverse_db(const InvArgs<T> p) {
+__global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_db(const InvArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* const X = reinterpret_cast<T*>(smem) + p.hlpad_a;
@@ -776,7 +779,7 @@ __global__ void VW_FUSED_BOUNDS(NV, 6) k_inverse_db(const InvArgs<T> p) {
 // Single-buffer sequential-sum form for signals too long for two LDS buffers: ONE region is
 // time-shared (a_j -> approx branch -> d_j -> detail branch -> a_{j-1}); four barriers per level.
 template <typename T, int L, bool FMA, int NV>
-__global__ void VW_FUSED_BOUNDS(NV, 6) k_inverse_seq(const InvArgs<T> p) {
+__global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_seq(const InvArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* R = reinterpret_cast<T*>(smem) + p.hlpad_a;
