@@ -28,6 +28,14 @@ for s in $STEPS; do
         fatal $rc && break
       done
       grep -o '"value": [0-9.]*\|"kernels_ms": {[^}]*}\|VW_NV.*' gpurun_out/ab.log ;;
+    configs)  # the other BASELINE configs, one bench line each (no CPU baseline)
+      : > gpurun_out/configs.log
+      for c in ${CONFIGS:-sym8-denoise db8-stream coif5-f32}; do
+        timeout -k 10 240 python bench.py --config $c --no-cpu-baseline --steps ${CFG_STEPS:-10} --warmup 3 >> gpurun_out/configs.log 2>&1; rc=$?
+        echo "$c rc=$rc" >> gpurun_out/configs.log
+        fatal $rc && break
+      done
+      grep -o '"value": [0-9.]*\|"kernels_ms": {[^}]*}\|^[a-z0-9-]* rc=.*' gpurun_out/configs.log ;;
     prof)
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1; rc=$?
       tail -3 gpurun_out/prof.log; echo "prof rc=$rc" ;;
