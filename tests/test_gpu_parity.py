@@ -219,9 +219,10 @@ def test_swt_mutable_threshold_and_extract(engine):
 
 # ---- streaming -------------------------------------------------------------------------------------
 @pytest.mark.parametrize("boundary", [O.ZERO_PADDING, O.SYMMETRIC], ids=["Z", "S"])
-def test_streaming_blocks_match_whole_signal(engine, boundary):
+@pytest.mark.parametrize("blk,J", [(256, 3), (12000, 5)])   # 12000 > fused capacity: per-level path + sweeps
+def test_streaming_blocks_match_whole_signal(engine, boundary, blk, J):
     w = Daubechies.DB4
-    J, blk, nb = 3, 256, 4
+    nb = 4 if blk <= 4096 else 2
     x = signals(2, blk * nb, 8)
     st = vw.BatchStreamingMODWT(w, vw.BoundaryMode(boundary), J)
     outs = [st.processMultiLevel(x[:, k * blk:(k + 1) * blk]) for k in range(nb)]
@@ -274,8 +275,11 @@ def test_fp32_path(engine):
 # ---- tiled (long-signal) path ---------------------------------------------------------------------------
 def test_tiled_path_bit_exact(engine, monkeypatch):
     monkeypatch.setenv("VW_FORCE_TILED", "1")
+    # levels with spacing >= 16 run as column sweeps (N % s != 0 exercises wraps across residues)
     for w, boundary, n, J in [(Daubechies.DB4, O.PERIODIC, 10000, 6), (Daubechies.DB8, O.SYMMETRIC, 5000, 4),
-                              (Symlet.SYM8, O.ZERO_PADDING, 9000, 5)]:
+                              (Symlet.SYM8, O.ZERO_PADDING, 9000, 5), (Daubechies.DB8, O.SYMMETRIC, 7001, 6),
+                              (Coiflet.COIF5, O.PERIODIC, 20000, 6),
+                              (Daubechies.DB4, O.SYMMETRIC, 4099, 8)]:
         x = signals(2, n, 19)
         tx = vw.MultiLevelMODWTTransform(w, vw.BoundaryMode(boundary))
         res = tx.decompose(x, J)

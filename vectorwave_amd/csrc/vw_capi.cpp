@@ -404,6 +404,16 @@ static bool fused_plan(int64_t N, int V, int elem, int64_t lds_elems_extra, int*
   return true;
 }
 
+// q-chunk per column-sweep thread (VW_SWEEP_QC overrides, for tuning)
+static int sweep_chunk() {
+  static const int qc = [] {
+    const char* e = getenv("VW_SWEEP_QC");
+    const int v = e ? atoi(e) : kSweepChunk;
+    return v >= 16 ? v : kSweepChunk;
+  }();
+  return qc;
+}
+
 // Owner-written halo of one level (vw_device.h halo_images): the affine images of an element and
 // the vector bands that have them; `own` only when every band lies in the slab that checks it.
 static void set_halo_images(LevelDesc& d, int64_t N, int64_t npow2, int V, int threads, int nv) {
@@ -504,9 +514,11 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
       if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward launch failed: %s", hipGetErrorString(e));
     }
   } else {
-    // Tiled per-level path: ping-pong the running approximation through the workspace.
-    if (hist) return fail(VW_ERR_UNSUPPORTED, "streaming blocks longer than the fused kernel holds in LDS");
-    const int tile_max = 256 * kNV * V;
+    // Per-level path for long signals: ping-pong the running approximation through the workspace.
+    // Deep levels (s >= kSweepMinS) run as column sweeps, shallow ones as LDS tiles with a halo.
+    for (int j = 1; hist && j <= J; ++j)
+      if (lv[j - 1].hist_len > N) return fail(VW_ERR_UNSUPPORTED, "streaming block shorter than level %d history", j);
+    const int tile_max = getenv("VW_FWD_TILE") ? atoi(getenv("VW_FWD_TILE")) / V * V : 256 * kNV * V;
     const size_t plane = (size_t)B * (size_t)N;
     const vw_status st = ensure_ws(c, 2 * plane * sizeof(T) + 256);
     if (st != VW_OK) return st;
@@ -529,14 +541,28 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
       a.out_d = details + (size_t)(j - 1) * plane;
       a.hist = hist ? hist[j - 1] : nullptr;
       a.B = B; a.N = (int)N; a.tile = tile; a.hlpad = hp;
-      a.vec_io = (N % V == 0) && aligned16(a.out_a) && aligned16(a.out_d);
+      a.vec_io = (N % V == 0) && (lda % V == 0) && aligned16(src) && aligned16(a.out_a) && aligned16(a.out_d);
       a.validate = validate; a.bad = c->bad; a.npow2 = npow2; a.taps = L;
       copy_taps(a.lo, lo, L);
       copy_taps(a.hi, hi, L);
+      const bool sweep = a.lv.s >= kSweepMinS && has_unrolled_taps(L) && !getenv("VW_NO_SWEEP");
       {
         LaunchTimer lt(c, "forward_level");
-        hipError_t e = launch_forward_level<T>(a, (int)(elems * sizeof(T)), fma, c->stream);
+        hipError_t e;
+        if (sweep) {
+          a.tile = sweep_chunk();
+          e = launch_forward_sweep<T>(a, fma, c->stream);
+        } else {
+          e = launch_forward_level<T>(a, (int)(elems * sizeof(T)), fma, c->stream);
+        }
         if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward level launch failed: %s", hipGetErrorString(e));
+      }
+      // streaming: this level's new left history = the last L_j - 1 samples of its input
+      // (BatchStreamingMODWT.updateHistoryFromSoA :337-352); read by this level's kernel first
+      if (hist && hist_update) {
+        hipError_t e = launch_history_update<T>(src, lda, hist[j - 1], hist[j - 1], B, (int)N, a.lv.hist_len,
+                                                c->stream);
+        if (e != hipSuccess) return fail(VW_ERR_DEVICE, "history update failed: %s", hipGetErrorString(e));
       }
       src = a.out_a;
       lda = N;
@@ -627,7 +653,9 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     hipError_t e = launch_inverse_fused<T>(a, threads, lds, fma, nv, c->stream);
     if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse launch failed: %s", hipGetErrorString(e));
   } else {
-    const int tile_max = 256 * kNV * V;
+    // 1024-sample tiles: two LDS regions of ~9 KiB keep many workgroups per CU (measured best on
+    // MI355X for db8 2^20-sample blocks; VW_INV_TILE overrides)
+    const int tile_max = getenv("VW_INV_TILE") ? atoi(getenv("VW_INV_TILE")) / V * V : 1024;
     const size_t plane = (size_t)B * (size_t)N;
     const vw_status st = ensure_ws(c, 2 * plane * sizeof(T) + 256);
     if (st != VW_OK) return st;
@@ -648,11 +676,17 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       a.out_a = (j == 1) ? y : tmp[j & 1];
       a.B = B; a.N = (int)N; a.tile = tile; a.hlpad = hp; a.hlpad_d = hp; a.region_d = (int)reg;
       a.pair = pair; a.thr = thr; a.soft = soft; a.taps = L;
-      a.vec_io = (N % V == 0) && aligned16(a.out_a);
+      a.vec_io = (N % V == 0) && aligned16(a.out_a) && aligned16(a.src_a) && aligned16(a.src_d);
       copy_taps(a.lo, lo, L);
       copy_taps(a.hi, hi, L);
       LaunchTimer lt(c, "inverse_level");
-      hipError_t e = launch_inverse_level<T>(a, (int)(2 * reg * sizeof(T)), fma, c->stream);
+      hipError_t e;
+      if (a.lv.s >= kSweepMinS && has_unrolled_taps(L) && !getenv("VW_NO_SWEEP")) {
+        a.tile = sweep_chunk();
+        e = launch_inverse_sweep<T>(a, fma, c->stream);
+      } else {
+        e = launch_inverse_level<T>(a, (int)(2 * reg * sizeof(T)), fma, c->stream);
+      }
       if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse level launch failed: %s", hipGetErrorString(e));
       cur = a.out_a;
     }

@@ -838,9 +838,30 @@ __device__ __forceinline__ T halo_value_global(const T* __restrict__ src, int id
 template <typename T>
 __device__ __forceinline__ void tile_to_lds(T* buf, const T* __restrict__ src, int N, int ts, int lo_q, int hi_q,
                                             int mode, int npow2, const T* hist_b, int hist_len, const T* thr,
-                                            T thr_b, int soft, bool zero) {
-  // buf[q] = value at signal index ts + q, q in [lo_q, hi_q)
-  for (int q = lo_q + (int)threadIdx.x; q < hi_q; q += blockDim.x) {
+                                            T thr_b, int soft, bool zero, bool vec_ok = false) {
+  // buf[q] = value at signal index ts + q, q in [lo_q, hi_q).  The in-range middle moves as 16-byte
+  // vectors (ts and the vector bounds are multiples of V; rows 16-B aligned when vec_ok); the
+  // ends go through the index map element by element.
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  int qa = lo_q, qb = lo_q;  // vector range [qa, qb)
+  if (vec_ok && !zero) {
+    qa = max(lo_q, -ts);
+    qa = (qa + V - 1) / V * V;
+    qb = min(hi_q, N - ts);
+    qb = qb >= qa ? qa + (qb - qa) / V * V : qa;
+  }
+  for (int q = qa + (int)threadIdx.x * V; q < qb; q += blockDim.x * V) {
+    vec v = __builtin_nontemporal_load(reinterpret_cast<const vec*>(src + ts + q));
+    if (thr) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) v[e] = threshold_t(v[e], thr_b, soft);
+    }
+    *reinterpret_cast<vec*>(buf + q) = v;
+  }
+  const int tail = (hi_q - lo_q) - (qb - qa);
+  for (int r = (int)threadIdx.x; r < tail; r += blockDim.x) {
+    const int q = (lo_q + r < qa) ? lo_q + r : qb + (r - (qa - lo_q));
     T v = zero ? T(0) : halo_value_global(src, ts + q, N, mode, npow2, hist_b, hist_len);
     if (thr) v = threshold_t(v, thr_b, soft);
     buf[q] = v;
@@ -861,7 +882,7 @@ __global__ void __launch_bounds__(256) k_forward_level(const LevelArgs<T> p) {
   const T* src = p.src_a + b * p.lda;
   const T* hist_b = (lv.mode == kHaloHistory) ? p.hist + b * lv.hist_len : nullptr;
   tile_to_lds(buf, src, N, ts, -lv.hl, nv * V, lv.mode, p.npow2, hist_b, lv.hist_len, (const T*)nullptr, T(0), 0,
-              false);
+              false, p.vec_io != 0 && (p.lda % V) == 0);
   if (p.validate) {
     for (int q = threadIdx.x; q < cnt; q += blockDim.x)
       if (!finite_t(buf[q])) atomicMin(p.bad, (unsigned long long)b * N + ts + q);
@@ -896,9 +917,9 @@ __global__ void __launch_bounds__(256) k_inverse_level(const LevelArgs<T> p) {
   const T thr_b = p.thr ? p.thr[b] : T(0);
   const int span = nv * V;
   tile_to_lds(A, p.src_a + b * (size_t)N, N, ts, -lv.hl, span + lv.hr, lv.mode, 0, (const T*)nullptr, 0,
-              (const T*)nullptr, T(0), 0, p.src_a == nullptr);
+              (const T*)nullptr, T(0), 0, p.src_a == nullptr, p.vec_io != 0);
   tile_to_lds(D, p.src_d + b * (size_t)N, N, ts, -lv.hl, span + lv.hr, lv.mode, 0, (const T*)nullptr, 0, p.thr,
-              thr_b, p.soft, p.use_d == 0 || p.src_d == nullptr);
+              thr_b, p.soft, p.use_d == 0 || p.src_d == nullptr, p.vec_io != 0);
   __syncthreads();
   const bool vec_ok = p.vec_io != 0;
   for (int w = threadIdx.x; w < nv; w += blockDim.x) {
@@ -913,6 +934,179 @@ __global__ void __launch_bounds__(256) k_inverse_level(const LevelArgs<T> p) {
       inv_branch<T, L, FMA>(D, t0, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
     }
     store_vec(p.out_a + b * (size_t)N + ts, t0, cnt, vec_ok, acc);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Column-sweep kernels for deep levels of long signals (spacing s >= kSweepMinS).  At spacing s
+// the level's convolution never mixes residues mod s: view the row as a matrix [N/s][s] and every
+// column r is an independent dense L-tap filter over q (t = r + q*s).  One thread owns one column
+// and a chunk of QC consecutive q, keeping the L most recent inputs in a register window: each
+// input is read from HBM once (+ L-1 warm-up reads per chunk), lanes read consecutive residues
+// (>= 128 contiguous bytes per lane group), and there is no LDS halo -- which at level 10 of db8
+// (15 x 512 = 7,680 samples) tripled the tiled kernel's reads.  Elements outside [0, N) (warm-up,
+// wrap, tail) go through the reference's index map (halo_value_global), so every boundary mode and
+// any N (wraps that change residue when s does not divide N) is exact; summation order per output
+// is the reference's (taps ascending; approximation branch, then detail branch).
+// kSweepMinS (vw_internal.h) = 16: 16 x 8 B = 128 B contiguous per lane group (fp64).
+
+struct SweepPos {
+  long long b;
+  int r, q0, q1;  // column r, q in [q0, q1)
+  bool ok;
+};
+
+__device__ __forceinline__ SweepPos sweep_pos(long long B, int N, int s, int qc) {
+  // thread -> (signal, chunk, residue), residue fastest: consecutive lanes = consecutive addresses
+  const int qn = (N + s - 1) / s;  // q extent of column 0
+  const int chunks = (qn + qc - 1) / qc;
+  const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long per = (long long)chunks * s;
+  SweepPos p;
+  p.b = g / per;
+  const long long rem = g - p.b * per;
+  const int c = (int)(rem / s);
+  p.r = (int)(rem - (long long)c * s);
+  const int qr = p.r < N ? (N - 1 - p.r) / s + 1 : 0;  // column r length
+  p.q0 = c * qc;
+  p.q1 = min(p.q0 + qc, qr);
+  p.ok = p.b < B && p.q0 < p.q1;
+  return p;
+}
+
+template <typename T>
+__device__ __forceinline__ T sweep_fetch(const T* __restrict__ src, long long u, int N, int mode, int npow2,
+                                         const T* hist_b, int hist_len) {
+  if (u >= 0 && u < N) return src[u];
+  return halo_value_global(src, (int)u, N, mode, npow2, hist_b, hist_len);
+}
+
+// Register window of one branch over a block of K outputs t_k = t_b + k*s (k < K):
+//   DIR = -1 (reads t - i*s + off):  w[j] = value at t_b + off + (j - (L-1))*s, tap i of output k = w[k - i + L - 1]
+//   DIR = +1 (reads t + i*s + off):  w[j] = value at t_b + off + j*s,           tap i of output k = w[k + i]
+// j in [0, K + L - 1).  Between blocks the last L - 1 values move to the front and K new values are
+// loaded -- all K loads of a block in flight at once (one load per output step would expose the
+// full memory latency per output).
+template <typename T, int L, int K, int DIR>
+struct SweepWin {
+  T w[K + L - 1];
+  __device__ __forceinline__ long long first(long long tb, int s, int off) const {
+    return tb + off + (DIR < 0 ? -(long long)(L - 1) * s : 0);
+  }
+  template <typename Fetch>
+  __device__ __forceinline__ void fill_head(long long tb, int s, int off, Fetch&& fetch) {  // j < L - 1
+    const long long u0 = first(tb, s, off);
+#pragma unroll
+    for (int j = 0; j < L - 1; ++j) w[j] = fetch(u0 + (long long)j * s);
+  }
+  template <typename Fetch>
+  __device__ __forceinline__ void load_block(long long tb, int s, int off, Fetch&& fetch) {  // j >= L - 1
+    const long long u0 = first(tb, s, off);
+#pragma unroll
+    for (int j = L - 1; j < K + L - 1; ++j) w[j] = fetch(u0 + (long long)j * s);
+  }
+  __device__ __forceinline__ void shift() {
+#pragma unroll
+    for (int j = 0; j < L - 1; ++j) w[j] = w[j + K];
+  }
+  __device__ __forceinline__ T tap(int k, int i) const { return DIR < 0 ? w[k - i + L - 1] : w[k + i]; }
+};
+
+// outputs per register block (loads in flight per branch); long filters keep their windows in budget
+template <int L> struct SweepK { static constexpr int K = L <= 16 ? 16 : 8; };
+
+// Forward, one level: a[t] = sum_i lo[i] x[g(t - i s)], d[t] likewise (ScalarOps.java:700-835 order).
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(256) k_forward_sweep(const LevelArgs<T> p) {
+  constexpr int K = SweepK<L>::K;
+  const LevelDesc lv = p.lv;
+  const int s = lv.s, N = p.N;
+  const SweepPos sp = sweep_pos(p.B, N, s, p.tile);
+  if (!sp.ok) return;
+  const T* src = p.src_a + sp.b * p.lda;
+  const T* hist_b = (lv.mode == kHaloHistory) ? p.hist + sp.b * lv.hist_len : nullptr;
+  T* oa = p.out_a + sp.b * (size_t)N;
+  T* od = p.out_d + sp.b * (size_t)N;
+  const unsigned long long flat0 = (unsigned long long)sp.b * N;
+  // inputs at or beyond the column end are never used by a stored output: read them as zero
+  const long long tend = (long long)sp.r + (long long)sp.q1 * s;
+  auto fetch = [&](long long u) -> T {
+    if (u >= tend) return T(0);
+    return sweep_fetch(src, u, N, lv.mode, p.npow2, hist_b, lv.hist_len);
+  };
+  SweepWin<T, L, K, -1> X;
+  long long tb = (long long)sp.r + (long long)sp.q0 * s;
+  X.fill_head(tb, s, 0, fetch);
+  for (int q = sp.q0; q < sp.q1; q += K, tb += (long long)K * s) {
+    X.load_block(tb, s, 0, fetch);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (q + k < sp.q1) {
+        T al = T(0), ah = T(0);
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+          al = madd<FMA>(al, X.tap(k, i), p.lo[i]);
+          ah = madd<FMA>(ah, X.tap(k, i), p.hi[i]);
+        }
+        const long long t = tb + (long long)k * s;
+        oa[t] = al;
+        od[t] = ah;
+        if (p.validate) {
+          if (!finite_t(X.tap(k, 0))) atomicMin(p.bad, flat0 + t);
+          if (!finite_t(al) || !finite_t(ah)) atomicMin(p.bad, (1ull << 62) | (flat0 + t));
+        }
+      }
+    }
+    X.shift();
+  }
+}
+
+// Inverse, one level: approximation branch (lo, dir_a, off_a) and detail branch (hi, dir_d, off_d),
+// each its own register window; sums in the reference's order (K4/K6 sequential, K5 pairwise).
+template <typename T, int L, bool FMA, int DA, int DD>
+__global__ void __launch_bounds__(256) k_inverse_sweep(const LevelArgs<T> p) {
+  constexpr int K = SweepK<L>::K;
+  const LevelDesc lv = p.lv;
+  const int s = lv.s, N = p.N;
+  const SweepPos sp = sweep_pos(p.B, N, s, p.tile);
+  if (!sp.ok) return;
+  const T thr_b = p.thr ? p.thr[sp.b] : T(0);
+  const T* sa = p.src_a ? p.src_a + sp.b * (size_t)N : nullptr;
+  const T* sd = p.src_d ? p.src_d + sp.b * (size_t)N : nullptr;
+  const bool za = sa == nullptr, zd = sd == nullptr || p.use_d == 0;
+  T* y = p.out_a + sp.b * (size_t)N;
+  auto fa = [&](long long u) -> T { return za ? T(0) : sweep_fetch(sa, u, N, lv.mode, 0, (const T*)nullptr, 0); };
+  auto fd = [&](long long u) -> T {
+    if (zd) return T(0);
+    const T v = sweep_fetch(sd, u, N, lv.mode, 0, (const T*)nullptr, 0);
+    return p.thr ? threshold_t(v, thr_b, p.soft) : v;
+  };
+  SweepWin<T, L, K, DA> A;
+  SweepWin<T, L, K, DD> D;
+  long long tb = (long long)sp.r + (long long)sp.q0 * s;
+  A.fill_head(tb, s, lv.off_a, fa);
+  D.fill_head(tb, s, lv.off_d, fd);
+  for (int q = sp.q0; q < sp.q1; q += K, tb += (long long)K * s) {
+    A.load_block(tb, s, lv.off_a, fa);
+    D.load_block(tb, s, lv.off_d, fd);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if (q + k < sp.q1) {
+        T acc = T(0);
+        if (p.pair) {  // MODWTTransform.inverse / K5: sum += h*a + g*d per tap
+#pragma unroll
+          for (int i = 0; i < L; ++i) acc = acc + pair_term<T, FMA>(p.lo[i], A.tap(k, i), p.hi[i], D.tap(k, i));
+        } else {       // K4 / K6: all approximation taps, then all detail taps
+#pragma unroll
+          for (int i = 0; i < L; ++i) acc = madd<FMA>(acc, A.tap(k, i), p.lo[i]);
+#pragma unroll
+          for (int i = 0; i < L; ++i) acc = madd<FMA>(acc, D.tap(k, i), p.hi[i]);
+        }
+        y[tb + (long long)k * s] = acc;
+      }
+    }
+    A.shift();
+    D.shift();
   }
 }
 

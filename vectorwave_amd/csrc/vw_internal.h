@@ -11,6 +11,8 @@ constexpr int kMaxLevels = 24;  // batch semantics have no level cap; LDS / N bo
 constexpr int kNV = 8;          // max vectors (16 B each) held per thread in the fused kernels (NV = 4 or 8)
 constexpr int kMaxThreads = 1024;
 constexpr int kLdsBytes = 160 * 1024;
+constexpr int kSweepMinS = 16;    // per-level path: spacings >= this run as column sweeps (vw_device.h)
+constexpr int kSweepChunk = 128;  // q-chunk per sweep thread (measured: 128 beats 256 and 64)
 
 // Source of the values outside [0, N) of a level's input ("halo"), i.e. the reference's index map.
 enum HaloMode : int {
@@ -123,6 +125,10 @@ template <typename T>
 hipError_t launch_forward_level(const LevelArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
 template <typename T>
 hipError_t launch_inverse_level(const LevelArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
+template <typename T>
+hipError_t launch_forward_sweep(const LevelArgs<T>& a, bool fma, hipStream_t st);
+template <typename T>
+hipError_t launch_inverse_sweep(const LevelArgs<T>& a, bool fma, hipStream_t st);
 template <typename T>
 hipError_t launch_history_update(const T* level_in, long long ld_in, const T* old_hist, T* new_hist,
                                  long long B, int n, int hist_len, hipStream_t st);

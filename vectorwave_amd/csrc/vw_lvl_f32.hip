@@ -56,6 +56,53 @@ static hipError_t dispatch_level(const LevelArgs<T>& a, int lds, bool fma, hipSt
   }
 }
 
+// Column sweeps (k_forward_sweep / k_inverse_sweep): one thread per (signal, column, q-chunk).
+template <typename T>
+static unsigned sweep_blocks(const LevelArgs<T>& a) {
+  const long long s = a.lv.s, qn = (a.N + s - 1) / s, chunks = (qn + a.tile - 1) / a.tile;
+  return (unsigned)((a.B * s * chunks + 255) / 256);
+}
+
+template <typename T, int L, bool FMA>
+static hipError_t run_forward_sweep(const LevelArgs<T>& a, hipStream_t st) {
+  hipLaunchKernelGGL((k_forward_sweep<T, L, FMA>), dim3(sweep_blocks(a)), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+template <typename T, int L, bool FMA>
+static hipError_t run_inverse_sweep(const LevelArgs<T>& a, hipStream_t st) {
+  const dim3 g(sweep_blocks(a)), blk(256);
+  const int da = a.lv.dir_a > 0, dd = a.lv.dir_d > 0;
+  if (da && dd) hipLaunchKernelGGL((k_inverse_sweep<T, L, FMA, 1, 1>), g, blk, 0, st, a);
+  else if (da) hipLaunchKernelGGL((k_inverse_sweep<T, L, FMA, 1, -1>), g, blk, 0, st, a);
+  else if (dd) hipLaunchKernelGGL((k_inverse_sweep<T, L, FMA, -1, 1>), g, blk, 0, st, a);
+  else hipLaunchKernelGGL((k_inverse_sweep<T, L, FMA, -1, -1>), g, blk, 0, st, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_forward_sweep(const LevelArgs<T>& a, bool fma, hipStream_t st) {
+  switch (a.taps) {
+#define VW_CASE(n) \
+    case n: return fma ? run_forward_sweep<T, n, true>(a, st) : run_forward_sweep<T, n, false>(a, st);
+    VW_TAP_LIST(VW_CASE)
+#undef VW_CASE
+    default: return hipErrorInvalidValue;  // runtime-L filters use the tiled kernel
+  }
+}
+template <typename T>
+hipError_t launch_inverse_sweep(const LevelArgs<T>& a, bool fma, hipStream_t st) {
+  switch (a.taps) {
+#define VW_CASE(n) \
+    case n: return fma ? run_inverse_sweep<T, n, true>(a, st) : run_inverse_sweep<T, n, false>(a, st);
+    VW_TAP_LIST(VW_CASE)
+#undef VW_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+template hipError_t launch_forward_sweep<VW_T>(const LevelArgs<VW_T>&, bool, hipStream_t);
+template hipError_t launch_inverse_sweep<VW_T>(const LevelArgs<VW_T>&, bool, hipStream_t);
+
 template <typename T>
 hipError_t launch_forward_level(const LevelArgs<T>& a, int lds, bool fma, hipStream_t st) {
   return dispatch_level<T, false>(a, lds, fma, st);
