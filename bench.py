@@ -51,6 +51,8 @@ def parse():
                    help="headline in EXACT accumulation (bit-identical to vectorwave-core) instead of FMA")
     p.add_argument("--fma", action="store_true", help="(default) FMA accumulation, max-abs error < 1e-12")
     p.add_argument("--no-alt", action="store_true", help="skip the timing of the other accumulation mode")
+    p.add_argument("--events", default="separate", choices=["inline", "separate"],
+                   help="HIP events around each kernel inside the timed region, or in a replay after it")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU baseline sample")
     return p.parse_args()
@@ -127,7 +129,7 @@ def main():
     torch.cuda.synchronize()
 
     eng.reset_timing()
-    eng.enable_timing(True)
+    eng.enable_timing(args.events == "inline")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -140,6 +142,13 @@ def main():
     t1 = time.perf_counter()
     eng.enable_timing(False)
     elapsed = t1 - t0
+    if args.events == "separate":
+        # per-kernel HIP-event durations from an instrumented replay of the same K steps
+        eng.enable_timing(True)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        eng.enable_timing(False)
     if world > 1:
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -230,6 +239,10 @@ def main():
                 "accumulation": ACC_NAME[bool(flags & nat.FLAG_FMA)],
                 "parallelism": f"batch-shard x{world} (no collective)",
                 "kernels_ms": {k: round(v[0], 5) for k, v in fam.items()},
+                "kernel_timing": ("HIP events on the engine stream around each launch, "
+                                  + ("inside the timed loop" if args.events == "inline" else
+                                     "in a replay of the K timed steps right after the (uninstrumented) timed loop")),
+                "kernel_ms_per_step": round(sum(v[0] * v[1] for v in fam.values()) / args.steps, 5),
                 "other_accumulation": alt,
             },
             "roofline": {

@@ -501,6 +501,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     a.vec_io = (ldx % V == 0) && (N % V == 0) && aligned16(x) && aligned16(details) && aligned16(approx);
     a.unrolled = a.vec_io && fit;
     a.validate = validate; a.bad = c->bad;
+    a.rev = getenv("VW_FWD_REV") ? atoi(getenv("VW_FWD_REV")) : 0;
     for (int j = 0; j < J; ++j) a.hist[j] = hist ? hist[j] : nullptr;
     a.hist_update = hist_update ? 1 : 0;
     a.taps = L;
@@ -646,6 +647,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     a.vec_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
     a.unrolled = a.vec_io && fit;
     a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.soft = soft; a.taps = L;
+    a.rev = getenv("VW_INV_REV") ? atoi(getenv("VW_INV_REV")) : 0;
     copy_taps(a.lo, lo, L);
     copy_taps(a.hi, hi, L);
     for (int j = 0; j < J; ++j) a.lv[j] = lv[j];

@@ -313,7 +313,46 @@ __device__ __forceinline__ void for_vecs(int nvec, F&& fn) {
   }
 }
 
-template <typename T>
+// Cache policy of the streaming row stores / loads (buffer-instruction aux field: 1 = sc0,
+// 2 = nt, 16 = sc1).  VW_STORE_AUX < 0 selects the compiler's nontemporal store.
+#ifndef VW_STORE_AUX
+#define VW_STORE_AUX -1
+#endif
+#ifndef VW_LOAD_AUX
+#define VW_LOAD_AUX -1
+#endif
+#ifndef VW_FWD_STORE_AUX
+#define VW_FWD_STORE_AUX VW_STORE_AUX  // forward coefficient rows (read next by an inverse)
+#endif
+#ifndef VW_INV_STORE_AUX
+#define VW_INV_STORE_AUX VW_STORE_AUX  // inverse output rows
+#endif
+typedef int vw_i4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t row_rsrc(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+
+// base: a workgroup-uniform row pointer; i: the lane's 16-byte vector index within the row.
+template <int AUX, typename V16, typename T>
+__device__ __forceinline__ void stream_store(T* base, int i, V16 v) {
+  if constexpr (AUX < 0) {
+    __builtin_nontemporal_store(v, reinterpret_cast<V16*>(base) + i);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(vw_i4, v), row_rsrc(base), i * 16, 0, AUX);
+  }
+}
+
+template <typename V16, typename T>
+__device__ __forceinline__ V16 stream_load(const T* base, int i) {
+  if constexpr (VW_LOAD_AUX < 0) {
+    return __builtin_nontemporal_load(reinterpret_cast<const V16*>(base) + i);
+  } else {
+    return __builtin_bit_cast(V16, __builtin_amdgcn_raw_buffer_load_b128(row_rsrc(base), i * 16, 0, VW_LOAD_AUX));
+  }
+}
+
+template <int AUX = VW_STORE_AUX, typename T>
 __device__ __forceinline__ void store_vec(T* __restrict__ dst, int t0, int N, bool vec_ok, const T (&v)[VT<T>::V]) {
   constexpr int V = VT<T>::V;
   using vec = typename VT<T>::v;
@@ -321,7 +360,7 @@ __device__ __forceinline__ void store_vec(T* __restrict__ dst, int t0, int N, bo
     vec o;
 #pragma unroll
     for (int e = 0; e < V; ++e) o[e] = v[e];
-    __builtin_nontemporal_store(o, reinterpret_cast<vec*>(dst + t0));
+    stream_store<AUX, vec>(dst, t0 / V, o);
   } else {
 #pragma unroll
     for (int e = 0; e < V; ++e)
@@ -371,7 +410,7 @@ __device__ __forceinline__ void load_row_regs(T (&r)[NV][VT<T>::V], const T* __r
       int w = (int)threadIdx.x + k * NT;
       asm volatile("" : "+v"(w));  // not hoisted out of the level loop (see for_vecs)
       w = min(w, nvec - 1);
-      const vec v = __builtin_nontemporal_load(reinterpret_cast<const vec*>(src + w * V));
+      const vec v = stream_load<vec>(src, w);
 #pragma unroll
       for (int e = 0; e < V; ++e) r[k][e] = v[e];
     }
@@ -610,8 +649,8 @@ __device__ __forceinline__ void fwd_level(const FwdArgs<T>& p, const T* X, int n
   const int N = p.N;
   fwd_row<T, L, FMA, NV>(X, nvec, lv.s, p.lo, p.hi, p.taps, [&](int k, int w, const T (&al)[V], const T (&ah)[V]) {
     const int t0 = w * V;
-    store_vec(dout, t0, N, vec_ok, ah);
-    if (aout) store_vec(aout, t0, N, vec_ok, al);
+    store_vec<VW_FWD_STORE_AUX>(dout, t0, N, vec_ok, ah);
+    if (aout) store_vec<VW_FWD_STORE_AUX>(aout, t0, N, vec_ok, al);
     if constexpr (VALIDATE) {
       check_out<T>(1, p.bad, flat0, t0, N, ah);
       check_out<T>(1, p.bad, flat0, t0, N, al);
@@ -628,7 +667,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_fused(const FwdA
   T* X = reinterpret_cast<T*>(smem) + p.hlpad;
   T* Y = p.region1 ? reinterpret_cast<T*>(smem) + p.region1 + p.hlpad : X;
   const bool dbl = p.region1 != 0;
-  const long long b = blockIdx.x;
+  const long long b = p.rev ? p.B - 1 - (long long)blockIdx.x : (long long)blockIdx.x;
   const int N = p.N;
   const int nvec = (N + V - 1) / V;
   const int NT = blockDim.x;
@@ -685,7 +724,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_fused(const InvA
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* A = reinterpret_cast<T*>(smem) + p.hlpad_a;
   T* D = reinterpret_cast<T*>(smem) + p.region_d + p.hlpad_d;
-  const long long b = blockIdx.x;
+  const long long b = p.rev ? p.B - 1 - (long long)blockIdx.x : (long long)blockIdx.x;
   const int N = p.N;
   const int nvec = (N + V - 1) / V;
   const bool vec_ok = (L > 0) || p.vec_io != 0;
@@ -722,7 +761,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_fused(const InvA
       }
     });
     if (j == 1) {
-      for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec(p.y + b * (size_t)N, w * V, N, vec_ok, reg[k]); });
+      for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, w * V, N, vec_ok, reg[k]); });
     } else {
       const LevelDesc ln = p.lv[j - 2];
       lds_barrier();  // all reads of A and D done
@@ -744,7 +783,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_db(const InvArgs
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* const X = reinterpret_cast<T*>(smem) + p.hlpad_a;
   T* const Y = reinterpret_cast<T*>(smem) + p.region_d + p.hlpad_d;
-  const long long b = blockIdx.x;
+  const long long b = p.rev ? p.B - 1 - (long long)blockIdx.x : (long long)blockIdx.x;
   const int N = p.N;
   const int nvec = (N + V - 1) / V;
   const bool vec_ok = (L > 0) || p.vec_io != 0;
@@ -773,7 +812,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_db(const InvArgs
     inv_row<T, L, FMA, NV>(Y, nvec, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
     if (j > 1) regs_to_level<T, L, NV>(X, acc, nvec, N, p.lv[j - 2], 0, (const T*)nullptr);
   }
-  for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec(p.y + b * (size_t)N, w * V, N, vec_ok, acc[k]); });
+  for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, w * V, N, vec_ok, acc[k]); });
 }
 
 // Single-buffer sequential-sum form for signals too long for two LDS buffers: ONE region is
@@ -783,7 +822,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_seq(const InvArg
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* R = reinterpret_cast<T*>(smem) + p.hlpad_a;
-  const long long b = blockIdx.x;
+  const long long b = p.rev ? p.B - 1 - (long long)blockIdx.x : (long long)blockIdx.x;
   const int N = p.N;
   const int nvec = (N + V - 1) / V;
   const bool vec_ok = (L > 0) || p.vec_io != 0;
@@ -816,7 +855,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_seq(const InvArg
       regs_to_level<T, L, NV>(R, acc, nvec, N, p.lv[j - 2], 0, (const T*)nullptr);
     }
   }
-  for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec(p.y + b * (size_t)N, w * V, N, vec_ok, acc[k]); });
+  for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, w * V, N, vec_ok, acc[k]); });
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -55,6 +55,7 @@ struct FwdArgs {
   int vec_io;
   int unrolled;         // 1: the tap-unrolled kernel may run (aligned rows, full slabs; vw_capi fused_plan)           // 1: rows and outputs are 16-B aligned -> vector global I/O
   int validate;         // 1: non-finite check on input and outputs (atomicMin into *bad)
+  int rev;              // 1: workgroup g owns signal B-1-g (walk order, see vw_capi.cpp walk_reverse)
   unsigned long long* bad;
   // streaming history (kHaloHistory): hist[j] is [B][hist_len_j], oldest first
   T* hist[kMaxLevels];
@@ -80,6 +81,7 @@ struct InvArgs {
   int unrolled;
   int db;               // sequential sum: 1 = two LDS buffers (k_inverse_db), 0 = one (k_inverse_seq)
   int approx_zero;
+  int rev;              // 1: workgroup g owns signal B-1-g
   const T* thr;         // per-signal threshold [B] (nullptr = no thresholding)
   int soft;
   int taps;
