@@ -583,9 +583,12 @@ void vwo_swt_reconstruct_periodic(const double *details, const double *approx, i
     free(h); free(g); free(cur); free(nxt);
 }
 
+/* Arrays.sort(double[]) order (Double.compare): NaN above +Inf, all NaNs equal.  The keys are |c|, so
+ * the -0.0 < 0.0 rule never applies. */
 static int cmp_double(const void *a, const void *b)
 {
     double x = *(const double *)a, y = *(const double *)b;
+    if (isnan(x) || isnan(y)) return (isnan(x) != 0) - (isnan(y) != 0);
     return (x > y) - (x < y);
 }
 

@@ -199,6 +199,37 @@ def test_noise_sigma_exact(engine):
             assert sig[b] == O.noise_sigma(c[b]), n
 
 
+def _sigma_cases(n, rng):
+    """Distributions that stress the selection kernel: ties, a single value, sub-normals, ranges spanning
+    the exponent range, keys a few ulps apart (many refinement passes), non-finite keys."""
+    one_ulp = np.spacing(1.0)
+    return {
+        "zeros": np.zeros(n),
+        "const": np.full(n, -3.25),
+        "two_values": np.where(rng.random(n) < 0.5, 1.0, 2.0),
+        "subnormal": rng.standard_normal(n) * 1e-310,
+        "wide": np.where(rng.random(n) < 0.5, 1e300, 1e-300) * rng.random(n),
+        "ulps": 1.0 + rng.integers(0, 5000, n) * one_ulp,
+        "ulps_narrow": 1.0 + rng.integers(0, 3, n) * one_ulp,
+        "outlier": np.concatenate([rng.standard_normal(n - 1) * 1e-12, [1e308]]),
+        "geometric": np.exp2(-rng.integers(0, 1000, n).astype(np.float64)),
+        "inf": np.where(np.arange(n) % 7 == 0, np.inf, rng.standard_normal(n)),
+        "nan": np.where(np.arange(n) % 3 == 0, np.nan, rng.standard_normal(n)),
+        "signed_zero": np.where(rng.random(n) < 0.6, -0.0, 0.0) + (np.arange(n) % 11 == 0) * 1.5,
+    }
+
+
+@pytest.mark.parametrize("n", [2, 7, 1000, 4096, 16383, 16384, 16385])
+def test_noise_sigma_adversarial(engine, n):
+    rng = np.random.default_rng(n)
+    cases = _sigma_cases(n, rng)
+    c = np.stack(list(cases.values()))
+    sig = vw.VectorWaveSwtAdapter(H).estimateNoiseSigma(c)
+    for b, name in enumerate(cases):
+        ref = O.noise_sigma(c[b])
+        assert np.array_equal(np.float64(sig[b]), np.float64(ref), equal_nan=True), (name, n, sig[b], ref)
+
+
 def test_swt_mutable_threshold_and_extract(engine):
     w = Daubechies.DB4
     x = signals(2, 512, 2)

@@ -275,6 +275,24 @@ def test_noise_sigma_median_even_odd():
     assert O.noise_sigma([1.0, -3.0, 2.0]) == 2.0 / 0.6745
 
 
+def test_noise_sigma_java_sort_order():
+    # Arrays.sort(double[]) (Double.compare): NaN sorts above +Inf, so a minority of NaNs leaves the median
+    # finite, and a median that reaches them is NaN.
+    nan, inf = float("nan"), float("inf")
+    assert O.noise_sigma([nan, 1.0, 2.0, nan, -3.0, 4.0, nan]) == 4.0 / 0.6745
+    assert O.noise_sigma([nan, -inf, 1.0]) == inf
+    assert math.isnan(O.noise_sigma([nan, nan, 1.0]))
+    assert O.noise_sigma([-0.0, 0.0, -0.0]) == 0.0
+    rng = np.random.default_rng(3)
+    for n in (10, 11, 1000):
+        c = rng.standard_normal(n)
+        c[rng.integers(0, n, n // 4)] = nan
+        key = np.sort(np.abs(c))  # numpy also sorts NaN last
+        med = (key[n // 2 - 1] + key[n // 2]) / 2.0 if n % 2 == 0 else key[n // 2]
+        got = O.noise_sigma(c)
+        assert (math.isnan(got) and math.isnan(med)) or got == med / 0.6745, n
+
+
 def test_threshold_soft_hard():
     # MutableMultiLevelMODWTResult.applyThresholdToArray :97-114
     c = [-3.0, -1.0, 0.0, 0.5, 2.0, 1.0]

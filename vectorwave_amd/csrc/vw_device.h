@@ -1159,105 +1159,6 @@ __global__ void k_history_update(const T* __restrict__ in, long long ld_in, cons
   new_hist[b * hist_len + p] = q >= 0 ? in[b * ld_in + q] : old_hist[b * hist_len + p + n];
 }
 
-// ---------------------------------------------------------------------------------------------
-// VectorWaveSwtAdapter.estimateNoiseSigma (:627-645): exact median of |c| by MSB-first radix
-// selection on the IEEE bit patterns (non-negative doubles order as unsigned integers), then
-// sigma = median / 0.6745 and the universal threshold T = sigma * sqrt(2 ln N) (:514).
-#ifdef VW_MISC_UNIT
-constexpr int kSigmaThreads = 1024;
-constexpr int kSigmaKeys = 16;
-
-__device__ __forceinline__ unsigned long long abs_bits(double v) {
-  return (unsigned long long)__double_as_longlong(v) & 0x7FFFFFFFFFFFFFFFull;
-}
-
-__global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __restrict__ coeffs, long long ld, int N,
-                                                               double scale_c, double* sigma_out, double* thr_out) {
-  __shared__ unsigned int hist[2][256];
-  __shared__ unsigned int wsum[2][kSigmaThreads / 64];
-  __shared__ unsigned long long prefix[2];
-  __shared__ long long krem[2];
-  const long long b = blockIdx.x;
-  const double* c = coeffs + b * ld;
-  const int tid = threadIdx.x;
-  const int nsel = (N % 2 == 0) ? 2 : 1;
-  const bool in_regs = N <= kSigmaThreads * kSigmaKeys;
-  unsigned long long keys[kSigmaKeys];
-  if (in_regs) {
-#pragma unroll
-    for (int k = 0; k < kSigmaKeys; ++k) {
-      const int i = tid + k * kSigmaThreads;
-      keys[k] = i < N ? abs_bits(c[i]) : 0ull;
-    }
-  }
-  if (tid == 0) {
-    prefix[0] = prefix[1] = 0ull;
-    krem[0] = (N % 2 == 0) ? N / 2 - 1 : N / 2;
-    krem[1] = N / 2;
-  }
-  for (int shift = 56; shift >= 0; shift -= 8) {
-    for (int q = tid; q < 512; q += kSigmaThreads) hist[q >> 8][q & 255] = 0u;
-    __syncthreads();
-    const unsigned long long hm = (shift == 56) ? 0ull : (~0ull << (shift + 8));
-    const unsigned long long p0 = prefix[0], p1 = prefix[1];
-    if (in_regs) {
-#pragma unroll
-      for (int k = 0; k < kSigmaKeys; ++k) {
-        const int i = tid + k * kSigmaThreads;
-        if (i < N) {
-          const unsigned long long key = keys[k];
-          const unsigned d = (unsigned)(key >> shift) & 255u;
-          if (((key ^ p0) & hm) == 0) atomicAdd(&hist[0][d], 1u);
-          if (nsel == 2 && ((key ^ p1) & hm) == 0) atomicAdd(&hist[1][d], 1u);
-        }
-      }
-    } else {
-      for (int i = tid; i < N; i += kSigmaThreads) {
-        const unsigned long long key = abs_bits(c[i]);
-        const unsigned d = (unsigned)(key >> shift) & 255u;
-        if (((key ^ p0) & hm) == 0) atomicAdd(&hist[0][d], 1u);
-        if (nsel == 2 && ((key ^ p1) & hm) == 0) atomicAdd(&hist[1][d], 1u);
-      }
-    }
-    __syncthreads();
-    // exclusive scan of 2 x 256 bins by threads 0..511 (wave-level shuffles)
-    const int r = tid >> 8, bin = tid & 255, lane = tid & 63, wv = (tid >> 6) & 3;
-    unsigned incl = 0;
-    if (tid < 512) {
-      const unsigned h = hist[r][bin];
-      incl = h;
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const unsigned t = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += t;
-      }
-      if (lane == 63) wsum[r][wv] = incl;
-    }
-    __syncthreads();
-    if (tid < 512 && r < nsel) {
-      unsigned base = 0;
-      for (int q = 0; q < wv; ++q) base += wsum[r][q];
-      const unsigned h = hist[r][bin];
-      const unsigned long long excl = (unsigned long long)(base + incl - h);
-      const long long k = krem[r];
-      if ((long long)excl <= k && k < (long long)(excl + h)) {
-        prefix[r] |= ((unsigned long long)bin) << shift;
-        krem[r] = k - (long long)excl;
-      }
-    }
-    __syncthreads();
-  }
-  if (tid == 0) {
-    const double v1 = __longlong_as_double((long long)prefix[0]);
-    const double v2 = __longlong_as_double((long long)prefix[1]);
-    const double median = (nsel == 2) ? (v1 + v2) / 2.0 : v1;
-    const double sigma = median / 0.6745;
-    if (sigma_out) sigma_out[b] = sigma;
-    if (thr_out) thr_out[b] = sigma * scale_c;
-  }
-}
-
-#endif  // VW_MISC_UNIT
 
 template <typename T>
 __global__ void k_threshold(T* c, long long B, long long N, const T* __restrict__ thr, int soft) {

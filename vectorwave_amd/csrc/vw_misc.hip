@@ -1,6 +1,7 @@
 // vw_misc.hip -- launchers (instantiation unit) for the kernels in vw_device.h.
 #define VW_MISC_UNIT 1
 #include "vw_device.h"
+#include "vw_sigma.h"
 
 namespace vw {
 

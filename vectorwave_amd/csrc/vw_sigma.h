@@ -1,0 +1,283 @@
+// vw_sigma.h -- per-signal noise estimate for the SWT denoise path (included by vw_misc.hip only).
+#pragma once
+#include "vw_device.h"
+
+namespace vw {
+
+// ---------------------------------------------------------------------------------------------
+// VectorWaveSwtAdapter.estimateNoiseSigma (:627-645): exact median of |c| by MSB-first radix
+// selection on the IEEE bit patterns (non-negative doubles order as unsigned integers), then
+// sigma = median / 0.6745 and the universal threshold T = sigma * sqrt(2 ln N) (:514).
+constexpr int kSigmaThreads = 1024;
+constexpr int kSigmaKeys = 16;
+
+__device__ __forceinline__ unsigned long long abs_bits(double v) {
+  return (unsigned long long)__double_as_longlong(v) & 0x7FFFFFFFFFFFFFFFull;
+}
+
+// Exact order statistics k1 = (N even ? N/2 - 1 : N/2) and k2 = N/2 of |c| by MSB-first radix selection (8-bit
+// digits).  Robust for any distribution (ties, zeros, non-finite values: NaN orders above +Inf as in
+// Arrays.sort), but a digit shared by most keys (the exponent byte) makes every key add into one LDS bin.
+__device__ __forceinline__ void radix_median(const double* __restrict__ c, int N, const unsigned long long (&keys)[kSigmaKeys],
+                                          bool in_regs, double* v1_out, double* v2_out) {
+  __shared__ unsigned int hist[2][256];
+  __shared__ unsigned int wsum[2][kSigmaThreads / 64];
+  __shared__ unsigned long long prefix[2];
+  __shared__ long long krem[2];
+  const int tid = threadIdx.x;
+  const int nsel = (N % 2 == 0) ? 2 : 1;
+  if (tid == 0) {
+    prefix[0] = prefix[1] = 0ull;
+    krem[0] = (N % 2 == 0) ? N / 2 - 1 : N / 2;
+    krem[1] = N / 2;
+  }
+  for (int shift = 56; shift >= 0; shift -= 8) {
+    for (int q = tid; q < 512; q += kSigmaThreads) hist[q >> 8][q & 255] = 0u;
+    __syncthreads();
+    const unsigned long long hm = (shift == 56) ? 0ull : (~0ull << (shift + 8));
+    const unsigned long long p0 = prefix[0], p1 = prefix[1];
+    if (in_regs) {
+#pragma unroll
+      for (int k = 0; k < kSigmaKeys; ++k) {
+        const int i = tid + k * kSigmaThreads;
+        if (i < N) {
+          const unsigned long long key = keys[k];
+          const unsigned d = (unsigned)(key >> shift) & 255u;
+          if (((key ^ p0) & hm) == 0) atomicAdd(&hist[0][d], 1u);
+          if (nsel == 2 && ((key ^ p1) & hm) == 0) atomicAdd(&hist[1][d], 1u);
+        }
+      }
+    } else {
+      for (int i = tid; i < N; i += kSigmaThreads) {
+        const unsigned long long key = abs_bits(c[i]);
+        const unsigned d = (unsigned)(key >> shift) & 255u;
+        if (((key ^ p0) & hm) == 0) atomicAdd(&hist[0][d], 1u);
+        if (nsel == 2 && ((key ^ p1) & hm) == 0) atomicAdd(&hist[1][d], 1u);
+      }
+    }
+    __syncthreads();
+    // exclusive scan of 2 x 256 bins by threads 0..511 (wave-level shuffles)
+    const int r = tid >> 8, bin = tid & 255, lane = tid & 63, wv = (tid >> 6) & 3;
+    unsigned incl = 0;
+    if (tid < 512) {
+      const unsigned h = hist[r][bin];
+      incl = h;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      if (lane == 63) wsum[r][wv] = incl;
+    }
+    __syncthreads();
+    if (tid < 512 && r < nsel) {
+      unsigned base = 0;
+      for (int q = 0; q < wv; ++q) base += wsum[r][q];
+      const unsigned h = hist[r][bin];
+      const unsigned long long excl = (unsigned long long)(base + incl - h);
+      const long long k = krem[r];
+      if ((long long)excl <= k && k < (long long)(excl + h)) {
+        prefix[r] |= ((unsigned long long)bin) << shift;
+        krem[r] = k - (long long)excl;
+      }
+    }
+    __syncthreads();
+  }
+  *v1_out = __longlong_as_double((long long)prefix[0]);
+  *v2_out = __longlong_as_double((long long)prefix[1]);
+}
+
+// Block-wide min / max over 1024 threads (16 waves): wave butterflies, then the 16 partials via LDS.
+__device__ __forceinline__ double block_minmax(double v, bool is_max, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double t = __shfl_xor(v, o, 64);
+    v = is_max ? (t > v ? t : v) : (t < v ? t : v);
+  }
+  __syncthreads();  // red[] free (previous use complete)
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = red[0];
+#pragma unroll
+  for (int q = 1; q < kSigmaThreads / 64; ++q) r = is_max ? (red[q] > r ? red[q] : r) : (red[q] < r ? red[q] : r);
+  return r;
+}
+
+constexpr int kSelBins = 2048;  // value buckets per refinement pass
+constexpr int kSelCand = 1024;  // a bucket this small is finished by exact ranking (one candidate per thread)
+
+// VectorWaveSwtAdapter.estimateNoiseSigma (:627-645) for N <= 16384, keys held in registers.
+// Selection by value-range refinement: bucket(v) = min(B-1, floor((v - lo) * B / (hi - lo))) is monotone
+// in v, so the keys of one bucket form a contiguous value interval; the bucket holding rank k is either
+// small (its keys are ranked exactly, in LDS) or becomes the next [lo, hi].  Two ranks in adjacent
+// buckets are the max of the first and the min of the second.  The result is the exact order statistic
+// (the same as sorting); anything unusual (non-finite keys, a range too narrow to scale, no
+// convergence in 6 passes) falls back to radix_median.  Two histogram atomics per key per pass on a
+// spread-out digit, instead of eight radix passes whose first digits every key shares.
+__global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __restrict__ coeffs, long long ld, int N,
+                                                               double scale_c, double* sigma_out, double* thr_out) {
+  __shared__ unsigned int hist[kSelBins];
+  __shared__ double cand[kSelCand];
+  __shared__ double red[kSigmaThreads / 64];
+  __shared__ unsigned int wsum[kSigmaThreads / 64];
+  __shared__ long long sel[2][3];  // per rank: bucket, exclusive count, count
+  __shared__ double res[2];
+  __shared__ int ncand;
+  const long long b = blockIdx.x;
+  const double* c = coeffs + b * ld;
+  const int tid = threadIdx.x;
+  const bool in_regs = N <= kSigmaThreads * kSigmaKeys;
+  const long long k1 = (N % 2 == 0) ? N / 2 - 1 : N / 2, k2 = N / 2;
+  unsigned long long keys[kSigmaKeys];
+  double v1 = 0.0, v2 = 0.0;
+  bool done = false;
+  if (in_regs) {
+    const bool vec = (N % 2 == 0) && (ld % 2 == 0) && ((reinterpret_cast<uintptr_t>(coeffs) & 15) == 0);
+    if (vec) {
+      typedef double d2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int k = 0; k < kSigmaKeys / 2; ++k) {
+        const int w = min(tid + k * kSigmaThreads, N / 2 - 1);
+        const d2 v = __builtin_nontemporal_load(reinterpret_cast<const d2*>(c) + w);
+        keys[2 * k] = abs_bits(v[0]);
+        keys[2 * k + 1] = abs_bits(v[1]);
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < kSigmaKeys / 2; ++k) {
+        const int i = 2 * (tid + k * kSigmaThreads);
+        keys[2 * k] = i < N ? abs_bits(c[i]) : 0ull;
+        keys[2 * k + 1] = i + 1 < N ? abs_bits(c[i + 1]) : 0ull;
+      }
+    }
+    // key slot 2k+e holds element 2*(tid + k*1024) + e
+    auto valid = [&](int q) { return 2 * (tid + (q >> 1) * kSigmaThreads) + (q & 1) < N; };
+    auto val = [&](int q) { return __longlong_as_double((long long)keys[q]); };
+    bool bad = false;
+    double lo = __builtin_inf(), hi = -__builtin_inf();
+#pragma unroll
+    for (int q = 0; q < kSigmaKeys; ++q) {
+      if (valid(q)) {
+        const double v = val(q);
+        bad |= !__builtin_isfinite(v);
+        lo = v < lo ? v : lo;
+        hi = v > hi ? v : hi;
+      }
+    }
+    bad = __syncthreads_or(bad);
+    lo = block_minmax(lo, false, red);
+    hi = block_minmax(hi, true, red);
+    long long r1 = k1, r2 = k2;  // ranks within the active keys [lo, hi]
+    for (int pass = 0; !bad && !done && pass < 6; ++pass) {
+      if (!(lo < hi)) { v1 = v2 = lo; done = true; break; }  // every active key equal
+      const double scale = (double)kSelBins / (hi - lo);
+      if (!__builtin_isfinite(scale)) break;
+      auto bucket = [&](double v) { return min(kSelBins - 1, (int)((v - lo) * scale)); };
+      for (int q = tid; q < kSelBins; q += kSigmaThreads) hist[q] = 0u;
+      __syncthreads();
+#pragma unroll
+      for (int q = 0; q < kSigmaKeys; ++q) {
+        const double v = val(q);
+        if (valid(q) && v >= lo && v <= hi) atomicAdd(&hist[bucket(v)], 1u);
+      }
+      __syncthreads();
+      // scan: thread t owns bins 2t, 2t+1
+      const unsigned h0 = hist[2 * tid], h1 = hist[2 * tid + 1];
+      unsigned incl = h0 + h1;
+      const int lane = tid & 63, wv = tid >> 6;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      if (lane == 63) wsum[wv] = incl;
+      __syncthreads();
+      unsigned base = 0;
+      for (int q = 0; q < wv; ++q) base += wsum[q];
+      const long long e0 = (long long)(base + incl - h0 - h1), e1 = e0 + h0;
+#pragma unroll
+      for (int r = 0; r < 2; ++r) {
+        const long long rk = r ? r2 : r1;
+        if (e0 <= rk && rk < e1) { sel[r][0] = 2 * tid; sel[r][1] = e0; sel[r][2] = h0; }
+        if (e1 <= rk && rk < e1 + h1) { sel[r][0] = 2 * tid + 1; sel[r][1] = e1; sel[r][2] = h1; }
+      }
+      if (tid == 0) ncand = 0;
+      __syncthreads();
+      const int b1 = (int)sel[0][0], b2 = (int)sel[1][0];
+      const long long ex1 = sel[0][1], cnt1 = sel[0][2];
+      auto in_bucket = [&](int q, int bk) {
+        const double v = val(q);
+        return valid(q) && v >= lo && v <= hi && bucket(v) == bk;
+      };
+      if (b1 != b2) {  // r2 = r1 + 1: the last key of bucket b1 and the first of bucket b2
+        double m1 = -__builtin_inf(), m2 = __builtin_inf();
+#pragma unroll
+        for (int q = 0; q < kSigmaKeys; ++q) {
+          const double v = val(q);
+          if (in_bucket(q, b1)) m1 = v > m1 ? v : m1;
+          if (in_bucket(q, b2)) m2 = v < m2 ? v : m2;
+        }
+        v1 = block_minmax(m1, true, red);
+        v2 = block_minmax(m2, false, red);
+        done = true;
+        break;
+      }
+      if (cnt1 <= kSelCand) {  // exact ranks inside the bucket
+#pragma unroll
+        for (int q = 0; q < kSigmaKeys; ++q)
+          if (in_bucket(q, b1)) cand[atomicAdd(&ncand, 1)] = val(q);
+        __syncthreads();
+        const int n = ncand;
+        if (tid < n) {
+          const double x = cand[tid];
+          int lt = 0, le = 0;
+          for (int j = 0; j < n; ++j) {
+            const double y = cand[j];
+            lt += y < x;
+            le += y <= x;
+          }
+          if (lt <= r1 - ex1 && r1 - ex1 < le) res[0] = x;
+          if (lt <= r2 - ex1 && r2 - ex1 < le) res[1] = x;
+        }
+        __syncthreads();
+        v1 = res[0];
+        v2 = res[1];
+        done = true;
+        break;
+      }
+      // refine: the next active range is bucket b1's [min, max]
+      double m1 = __builtin_inf(), m2 = -__builtin_inf();
+#pragma unroll
+      for (int q = 0; q < kSigmaKeys; ++q) {
+        const double v = val(q);
+        if (in_bucket(q, b1)) { m1 = v < m1 ? v : m1; m2 = v > m2 ? v : m2; }
+      }
+      const double nlo = block_minmax(m1, false, red);
+      const double nhi = block_minmax(m2, true, red);
+      lo = nlo;
+      hi = nhi;
+      r1 -= ex1;
+      r2 -= ex1;
+    }
+  }
+  if (!done) {
+    // radix fallback (also N > 16384): key slots hold element tid + k*1024 there
+    if (in_regs) {
+#pragma unroll
+      for (int k = 0; k < kSigmaKeys; ++k) {
+        const int i = tid + k * kSigmaThreads;
+        keys[k] = i < N ? abs_bits(c[i]) : 0ull;
+      }
+    }
+    radix_median(c, N, keys, in_regs, &v1, &v2);
+  }
+  if (tid == 0) {
+    const double median = (N % 2 == 0) ? (v1 + v2) / 2.0 : v1;  // odd N: k1 = N/2
+    const double sigma = median / 0.6745;
+    if (sigma_out) sigma_out[b] = sigma;
+    if (thr_out) thr_out[b] = sigma * scale_c;
+  }
+}
+
+
+}  // namespace vw
