@@ -285,6 +285,56 @@ def test_fma_variant_within_tolerance(engine):
                                                        O.PERIODIC), rtol=0, atol=1e-12)
 
 
+@pytest.mark.parametrize("case", [
+    ("db4", O.PERIODIC, 4096, 6, "f64", nat.FLAG_FMA, None),
+    ("db4", O.PERIODIC, 4096, 6, "f64", 0, "2"),          # EXACT on two buffers -> persistent, bit-exact
+    ("db4", O.SYMMETRIC, 4096, 5, "f64", nat.FLAG_FMA, None),
+    ("db4", O.ZERO_PADDING, 4096, 4, "f64", nat.FLAG_FMA, None),
+    ("sym8", O.PERIODIC, 4096, 6, "f64", nat.FLAG_FMA, None),
+    ("db4", O.PERIODIC, 1024, 3, "f64", nat.FLAG_FMA, "2"),
+    ("coif5", O.PERIODIC, 8192, 6, "f32", nat.FLAG_FMA, None),
+], ids=lambda c: f"{c[0]}-{c[1]}-{c[2]}-J{c[3]}-{c[4]}-{'fma' if c[5] else 'exact'}")
+def test_forward_persistent_matches_per_signal_kernel(engine, case):
+    """k_forward_persist (a workgroup walks several signals; the next row arrives by LDS-DMA during the
+    last level) against k_forward_fused (one signal per workgroup): identical arithmetic, so identical
+    bits, over a batch larger than the resident grid (every workgroup handles >= 2 signals)."""
+    import torch
+    wname, boundary, n, J, dt, flags, buf = case
+    w = {"db4": Daubechies.DB4, "sym8": Symlet.SYM8, "coif5": Coiflet.COIF5}[wname]
+    B = 1100 if n <= 4096 else 700
+    dtype = torch.float64 if dt == "f64" else torch.float32
+    x = torch.empty((B, n), dtype=dtype, device="cuda")
+    engine.fill_uniform(x, 5)
+    old = {k: os.environ.get(k) for k in ("VW_FWD_PERSIST", "VW_FWD_BUF")}
+    try:
+        if buf:
+            os.environ["VW_FWD_BUF"] = buf
+        outs = []
+        for persist in ("0", "1"):
+            os.environ["VW_FWD_PERSIST"] = persist
+            outs.append(engine.forward(x, *lohi(w), w.wavelet_id, boundary, J, flags))
+            torch.cuda.synchronize()
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    (d0, a0), (d1, a1) = outs
+    assert torch.equal(d0, d1) and torch.equal(a0, a1)
+    xh = x.double().cpu().numpy()
+    tol = 1e-12 if dt == "f64" else 2e-5 * J
+    for b in (0, 511, 512, B - 1):
+        d_ref, a_ref = O.decompose(xh[b], *lohi(w), boundary, J)
+        got_d, got_a = d1[:, b, :].double().cpu().numpy(), a1[b].double().cpu().numpy()
+        if dt == "f64" and not flags:
+            exact(got_d, d_ref)
+            exact(got_a, a_ref)
+        else:
+            np.testing.assert_allclose(got_d, d_ref, rtol=0, atol=tol)
+            np.testing.assert_allclose(got_a, a_ref, rtol=0, atol=tol)
+
+
 def test_fp32_path(engine):
     import torch
     w = Coiflet.COIF5

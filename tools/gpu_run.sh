@@ -37,7 +37,7 @@ for s in $STEPS; do
       done
       grep -o '"value": [0-9.]*\|"kernels_ms": {[^}]*}\|^[a-z0-9-]* rc=.*' gpurun_out/configs.log ;;
     prof)
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline --steps 10 --warmup 3 ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1; rc=$?
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --no-cpu-baseline ${BENCH_ARGS:-} > gpurun_out/prof.log 2>&1; rc=$?
       tail -3 gpurun_out/prof.log; echo "prof rc=$rc" ;;
     traffic)  # HBM bytes per launch (PMC FETCH_SIZE / WRITE_SIZE, separate passes) -> gpurun_out/hbm_traffic_<cfg>.json
       rm -rf gpurun_out/pmc

@@ -18,7 +18,7 @@ import sys
 
 def family(kernel):
     k = kernel.split("(")[0].replace("void ", "").replace("vw::", "").strip()
-    if k.startswith("k_forward_fused"):
+    if k.startswith("k_forward_fused") or k.startswith("k_forward_persist"):
         return "forward"
     if k.startswith("k_inverse_fused") or k.startswith("k_inverse_seq") or k.startswith("k_inverse_db"):
         return "inverse"

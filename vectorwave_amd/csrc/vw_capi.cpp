@@ -509,9 +509,18 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     copy_taps(a.hi, hi, L);
     for (int j = 0; j < J; ++j) a.lv[j] = lv[j];
     if (validate) VW_HIP(hipMemsetAsync(c->bad, 0xFF, sizeof(unsigned long long), c->stream));
+    // Persistent variant (vw_device.h k_forward_persist): next row by LDS-DMA during the last level.
+    // Its contract: two buffers, full slabs of whole waves, rows in 64-vector chunks, no validation
+    // or streaming history.  VW_FWD_PERSIST=0 disables it.
+    const char* pe = getenv("VW_FWD_PERSIST");
+    const bool persist_on = !pe || atoi(pe) != 0;
+    const bool persist = persist_on && dbl && a.unrolled && nv == 4 && !validate && !hist &&
+                         (int64_t)threads * nv == nvec && threads % 64 == 0 && nvec % 64 == 0 &&
+                         has_unrolled_taps(L) && J >= 1;
     {
       LaunchTimer lt(c, "forward");
-      hipError_t e = launch_forward_fused<T>(a, threads, lds, fma, nv, c->stream);
+      hipError_t e = persist ? launch_forward_persist<T>(a, threads, lds, fma, c->stream)
+                             : launch_forward_fused<T>(a, threads, lds, fma, nv, c->stream);
       if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward launch failed: %s", hipGetErrorString(e));
     }
   } else {
@@ -651,6 +660,9 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     copy_taps(a.lo, lo, L);
     copy_taps(a.hi, hi, L);
     for (int j = 0; j < J; ++j) a.lv[j] = lv[j];
+    // (A persistent form that loads the next signal's approximation during level 1 was measured
+    // slower on MI355X: 3 resident workgroups per CU do not divide the batch evenly, and the dynamic
+    // dispatch of one-signal workgroups balances better.)
     LaunchTimer lt(c, "inverse");
     hipError_t e = launch_inverse_fused<T>(a, threads, lds, fma, nv, c->stream);
     if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse launch failed: %s", hipGetErrorString(e));

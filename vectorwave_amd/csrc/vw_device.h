@@ -713,6 +713,89 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_fused(const FwdA
 }
 
 // ---------------------------------------------------------------------------------------------
+// Persistent fused forward: the same cascade as k_forward_fused, but each workgroup walks the
+// signals b = blockIdx.x, + gridDim.x, ... and copies the NEXT signal's row into LDS while the
+// current one computes its last level.  With two level buffers, level J reads X and writes no next
+// level, so the other buffer is free from its first barrier on: the row goes there by LDS-DMA
+// (global_load_lds_dwordx4, no VGPRs), overlapping the read of x with level J's arithmetic and
+// detail stores instead of starting every signal with an exposed load (one workgroup per signal
+// waits for its row before any store can be issued; at 2 workgroups per CU both often wait at once).
+//
+// The DMA is issued from inline asm so the compiler does not pessimistically wait for it before the
+// LDS reads of level J (it cannot prove the buffers disjoint).  Completion is waited for explicitly:
+// vmcnt counts a wave's vector-memory operations in issue order, and exactly 2*NV stores (detail +
+// approximation rows) follow the DMA, so vmcnt(2*NV) retires the DMA and leaves those stores in
+// flight.  Host contract (vw_capi.cpp): two buffers, every slab full (threads*NV == N/V), whole
+// waves, N/V a multiple of 64 (one wave instruction = 64 x 16 B), no validation, no history.
+template <typename T>
+__device__ __forceinline__ void dma_row(T* buf, const T* __restrict__ src, int nvec) {
+  constexpr int V = VT<T>::V;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int c = wv; c * 64 < nvec; c += nw) {
+    const T* g = src + (size_t)(c * 64 + lane) * V;
+    const unsigned lds = (unsigned)(uintptr_t)(buf + c * 64 * V);  // LDS byte address (wave-uniform)
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
+        : "memory");
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+template <typename T, int L, bool FMA, int NV>
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, NV <= 4 ? 512 : 1024), amdgpu_waves_per_eu(4)))
+k_forward_persist(const FwdArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* const B0 = reinterpret_cast<T*>(smem) + p.hlpad;  // (no pointer array: it would lose the LDS address space)
+  T* const B1 = reinterpret_cast<T*>(smem) + p.region1 + p.hlpad;
+  const int N = p.N;
+  const int nvec = N / V;
+  const long long G = gridDim.x;
+  long long b = blockIdx.x;
+  if (b >= p.B) return;
+  int cur = 0;
+  dma_row<T>(B0, p.x + b * p.ldx, nvec);
+  wait_vmem();
+  for (;;) {
+    T* X = cur ? B1 : B0;
+    T* Y = cur ? B0 : B1;
+    lds_barrier();  // the row is in X (every wave's share); every read of the previous signal done
+    const LevelDesc lv0 = p.lv[0];
+    fill_halo(X, N, lv0.hl, lv0.hr, lv0.mode, p.npow2, (const T*)nullptr, 0);
+    const long long bn = b + G;
+    T areg[NV][V];
+    for (int j = 1; j <= p.J; ++j) {
+      const LevelDesc lv = p.lv[j - 1];
+      lds_barrier();  // X = level input + halo; every read of Y (previous level) done
+      if (j == p.J && bn < p.B) dma_row<T>(Y, p.x + bn * p.ldx, nvec);  // next signal -> free buffer
+      T* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
+      T* aout = (j == p.J) ? p.approx + b * (size_t)N : nullptr;
+      fwd_level<T, L, FMA, NV, false>(p, X, nvec, lv, dout, aout, true, 0ull, areg);
+      if (j < p.J) {
+        regs_to_level<T, L, NV>(Y, areg, nvec, N, p.lv[j], p.npow2, (const T*)nullptr);
+        T* t = X; X = Y; Y = t;
+      }
+    }
+    if (bn >= p.B) break;
+    wait_vmcnt<2 * NV>();  // this wave's DMA share landed; level J's stores stay in flight
+    cur = (cur + p.J) & 1;  // the buffer that was free during level J
+    b = bn;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Fused multi-level inverse: MultiLevelMODWTTransform.reconstruct (:339-349, :554-645),
 // VectorWaveSwtAdapter.reconstructPeriodic (:444-474), MODWTTransform.inverse (J=1, pairwise),
 // with the denoise threshold (MutableMultiLevelMODWTResult.java:97-114) fused into the detail load.

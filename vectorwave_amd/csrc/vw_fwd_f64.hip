@@ -1,6 +1,7 @@
 #define VW_T double
 // vw_fwd_f64.hip -- launchers (instantiation unit) for the kernels in vw_device.h.
 #include "vw_device.h"
+#include <algorithm>
 
 namespace vw {
 
@@ -52,4 +53,38 @@ hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds, bool 
   }
 }
 template hipError_t launch_forward_fused<VW_T>(const FwdArgs<VW_T>&, int, int, bool, int, hipStream_t);
+// Persistent forward (k_forward_persist): as many workgroups as are resident at once, each walking
+// signals blockIdx.x + k*gridDim.x.  The resident count comes from the occupancy API (LDS-bound).
+template <typename T, int L, bool FMA>
+static hipError_t run_forward_persist(const FwdArgs<T>& a, int threads, int lds, hipStream_t st) {
+  auto k = k_forward_persist<T, L, FMA, 4>;
+  static int configured = 64 * 1024;
+  hipError_t e = set_lds(k, lds, &configured);
+  if (e != hipSuccess) return e;
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+  }
+  int per_cu = 0;
+  if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds)) != hipSuccess) return e;
+  if (per_cu < 1) return hipErrorInvalidConfiguration;
+  const long long grid = std::min<long long>(a.B, (long long)per_cu * cus);
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(threads), lds, st, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_forward_persist(const FwdArgs<T>& a, int threads, int lds, bool fma, hipStream_t st) {
+  switch (a.taps) {
+#define VW_CASE(n) \
+    case n: return fma ? run_forward_persist<T, n, true>(a, threads, lds, st) : run_forward_persist<T, n, false>(a, threads, lds, st);
+    VW_TAP_LIST(VW_CASE)
+#undef VW_CASE
+    default:
+      return hipErrorNotSupported;
+  }
+}
+template hipError_t launch_forward_persist<VW_T>(const FwdArgs<VW_T>&, int, int, bool, hipStream_t);
 }  // namespace vw

@@ -122,6 +122,8 @@ struct LevelArgs {
 template <typename T>
 hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
 template <typename T>
+hipError_t launch_forward_persist(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, hipStream_t st);
+template <typename T>
 hipError_t launch_inverse_fused(const InvArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
 template <typename T>
 hipError_t launch_forward_level(const LevelArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);

@@ -1,6 +1,7 @@
 #define VW_T float
 // vw_inv_f32.hip -- launchers (instantiation unit) for the kernels in vw_device.h.
 #include "vw_device.h"
+#include <algorithm>
 
 namespace vw {
 
