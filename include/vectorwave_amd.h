@@ -179,6 +179,25 @@ VW_API vw_status vw_swt_denoise_f64(vw_ctx *ctx, const double *x, int64_t B, int
                                     const double *lo, const double *hi, int L, int wavelet_id,
                                     int boundary, int J, double threshold, int soft, unsigned flags,
                                     double *y, double *thresholds_out);
+/* ---- WaveletDenoiser ---------------------------------------------------- */
+/* Replaces com.morphiqlabs.wavelet.denoising.WaveletDenoiser (core/denoising/WaveletDenoiser.java):
+ *   levels == 0, method != FIXED : denoise(signal, method, type)            :124-143
+ *   levels == 0, method == FIXED : denoiseFixed(signal, fixed_threshold, type) :354-364
+ *   levels >= 1                  : denoiseMultiLevel(signal, levels, method, type) :155-170, with
+ *                                  DenoisedMultiLevelResult's per-level thresholds :204-231
+ *                                  (sigma = MAD(d_1)/0.6745, level j uses sigma / sqrt(2^j)).
+ * method: VW_THR_* (calculateThreshold :394-436).  SURE needs N <= 16384 (VW_ERR_UNSUPPORTED).
+ * soft: 1 SOFT, 0 HARD.  thresholds_out (optional, [max(levels,1)][B], same memory kind as y). */
+#define VW_THR_UNIVERSAL 0
+#define VW_THR_SURE 1
+#define VW_THR_MINIMAX 2
+#define VW_THR_BAYES 3
+#define VW_THR_FIXED 4
+VW_API vw_status vw_wavelet_denoise_f64(vw_ctx *ctx, const double *x, int64_t B, int64_t N, int64_t ldx,
+                                        const double *lo, const double *hi, int L, int wavelet_id,
+                                        int boundary, int levels, int method, double fixed_threshold, int soft,
+                                        unsigned flags, double *y, double *thresholds_out);
+
 /* sigma[b] = median(|coeffs[b][:]|) / 0.6745 (exact selection, even N = mean of middle pair). */
 VW_API vw_status vw_noise_sigma_f64(vw_ctx *ctx, const double *coeffs, int64_t B, int64_t N,
                                     unsigned flags, double *sigma);

@@ -58,6 +58,13 @@ def lib() -> ctypes.CDLL:
             "vwo_modwt_forward": (c_int, [_dp, c_int, _dp, _dp, c_int, c_int, _dp, _dp, POINTER(c_longlong)]),
             "vwo_modwt_inverse": (c_int, [_dp, _dp, c_int, _dp, _dp, c_int, c_int, c_int, _dp]),
             "vwo_swt_forward": (c_int, [_dp, c_int, _dp, _dp, c_int, c_int, c_int, _dp, _dp]),
+            "vwo_sure_risk": (c_double, [_dp, c_int, c_double, c_double]),
+            "vwo_sure_threshold": (c_double, [_dp, c_int, c_double]),
+            "vwo_minimax_threshold": (c_double, [c_int, c_double]),
+            "vwo_bayes_threshold": (c_double, [_dp, c_int, c_double]),
+            "vwo_calc_threshold": (c_int, [_dp, c_int, c_double, c_int, _dp]),
+            "vwo_wavelet_denoise": (c_int, [_dp, c_int, _dp, _dp, c_int, c_int, c_int, c_int, c_int, c_double, c_int,
+                                            _dp, _dp, POINTER(c_longlong)]),
             "vwo_swt_reconstruct_periodic": (None, [_dp, _dp, c_int, _dp, _dp, c_int, c_int, _dp]),
             "vwo_noise_sigma": (c_double, [_dp, c_int]),
             "vwo_universal_threshold": (c_double, [c_double, c_int]),
@@ -275,3 +282,37 @@ def java_random_signal(n: int, seed: int) -> np.ndarray:
     """`new Random(seed).nextDouble() * 2 - 1` per sample, the reference tests' common input."""
     r = JavaRandom(seed)
     return np.array([r.nextDouble() * 2 - 1 for _ in range(n)])
+
+
+# ---- WaveletDenoiser (core/denoising/WaveletDenoiser.java) -----------------------------------------
+UNIVERSAL, SURE, MINIMAX, BAYES, FIXED = 0, 1, 2, 3, 4
+
+
+def calc_threshold(c, sigma: float, method: int) -> float:
+    """calculateThreshold :394-436 (SURE is the reference's O(n^2) search)."""
+    c = _arr(c)
+    out = c_double()
+    st = lib().vwo_calc_threshold(_p(c), len(c), sigma, method, ctypes.byref(out))
+    if st != 0:
+        raise OracleError(st)
+    return out.value
+
+
+def sure_risk(c, t: float, sigma: float) -> float:
+    c = _arr(c)
+    return lib().vwo_sure_risk(_p(c), len(c), t, sigma)
+
+
+def wavelet_denoise(x, lo, hi, boundary: int, levels: int, method: int, fixed: float = 0.0, soft: bool = True,
+                    wavelet_id: int = 0):
+    """WaveletDenoiser.denoise (levels == 0) / denoiseFixed (levels == 0, method FIXED) / denoiseMultiLevel.
+    Returns (y, thresholds[max(levels, 1)])."""
+    x, lo, hi = _arr(x), _arr(lo), _arr(hi)
+    y = np.empty(len(x))
+    thr = np.empty(max(levels, 1))
+    bad = c_longlong(-1)
+    st = lib().vwo_wavelet_denoise(_p(x), len(x), _p(lo), _p(hi), len(lo), wavelet_id, boundary, levels, method, fixed,
+                                   1 if soft else 0, _p(y), _p(thr), ctypes.byref(bad))
+    if st != 0:
+        raise OracleError(st, bad.value)
+    return y, thr

@@ -646,6 +646,122 @@ int vwo_swt_denoise(const double *x, int n, const double *lo, const double *hi, 
     return st;
 }
 
+/* ------------------------------------------------------- WaveletDenoiser ---- */
+/* core/denoising/WaveletDenoiser.java.  Methods: 0 UNIVERSAL, 1 SURE, 2 MINIMAX, 3 BAYES, 4 FIXED. */
+enum { VWO_THR_UNIVERSAL = 0, VWO_THR_SURE = 1, VWO_THR_MINIMAX = 2, VWO_THR_BAYES = 3, VWO_THR_FIXED = 4 };
+
+/* calculateSURERisk :477-492 -- sequential sum in coefficient order */
+double vwo_sure_risk(const double *c, int n, double threshold, double sigma)
+{
+    double sigma2 = sigma * sigma;
+    double risk = -n * sigma2;
+    for (int i = 0; i < n; i++) {
+        double absC = fabs(c[i]);
+        if (absC <= threshold) risk += c[i] * c[i];
+        else risk += sigma2 + (absC - threshold) * (absC - threshold);
+    }
+    return risk / n;
+}
+
+/* calculateSUREThreshold :441-472 -- every sorted |c| is tried (O(n^2)), first minimum kept, capped at
+ * the universal threshold */
+double vwo_sure_threshold(const double *c, int n, double sigma)
+{
+    double *s = malloc(sizeof(double) * (size_t)n);
+    for (int i = 0; i < n; i++) s[i] = fabs(c[i]);
+    qsort(s, n, sizeof(double), cmp_double);
+    double minRisk = INFINITY, best = 0;
+    for (int k = 0; k < n; k++) {
+        double t = s[k];
+        double risk = vwo_sure_risk(c, n, t, sigma);
+        if (risk < minRisk) { minRisk = risk; best = t; }
+    }
+    free(s);
+    double universal = sigma * sqrt(2.0 * log((double)n));
+    if (best > universal) best = universal;
+    return best;
+}
+
+/* calculateMinimaxThreshold :497-509 */
+double vwo_minimax_threshold(int n, double sigma)
+{
+    double logN = log((double)n);
+    if (n <= 32) return 0;
+    if (n <= 64) return sigma * 0.3936 + 0.1829 * sigma * logN;
+    return sigma * (0.4745 + 0.1148 * logN);
+}
+
+/* calculateBayesThreshold :521-549 -- sequential mean and variance, BAYES_EPSILON = 1e-10 (:62) */
+double vwo_bayes_threshold(const double *c, int n, double sigma)
+{
+    double sigma2 = sigma * sigma;
+    double mean = 0.0;
+    for (int i = 0; i < n; i++) mean += c[i];
+    mean /= n;
+    double variance = 0.0;
+    for (int i = 0; i < n; i++) {
+        double diff = c[i] - mean;
+        variance += diff * diff;
+    }
+    variance /= n;
+    double sigmaX2 = variance - sigma2 > 0.0 ? variance - sigma2 : 0.0; /* Math.max(0.0, v - s2), finite */
+    double sigmaX = sqrt(sigmaX2 + 1e-10);
+    return sigma2 / sigmaX;
+}
+
+/* calculateThreshold :394-436 (FIXED -> error) */
+int vwo_calc_threshold(const double *c, int n, double sigma, int method, double *out)
+{
+    switch (method) {
+        case VWO_THR_UNIVERSAL: *out = sigma * sqrt(2.0 * log((double)n)); return VWO_OK;
+        case VWO_THR_SURE: *out = vwo_sure_threshold(c, n, sigma); return VWO_OK;
+        case VWO_THR_MINIMAX: *out = vwo_minimax_threshold(n, sigma); return VWO_OK;
+        case VWO_THR_BAYES: *out = vwo_bayes_threshold(c, n, sigma); return VWO_OK;
+        default: return VWO_ERR_ARG;
+    }
+}
+
+/* denoise(signal, method, type) :124-143 (levels == 0; method FIXED = denoiseFixed :354-364 with
+ * `fixed`), denoiseMultiLevel :155-170 with DenoisedMultiLevelResult's per-level thresholds :204-231
+ * (sigma from d_1, level j uses sigma / Math.sqrt(1 << j) and its own coefficients).  thr_out holds
+ * max(levels, 1) thresholds. */
+int vwo_wavelet_denoise(const double *x, int n, const double *lo, const double *hi, int L, int wavelet_id,
+                        int boundary, int levels, int method, double fixed, int soft, double *y, double *thr_out,
+                        long long *bad_index)
+{
+    int st;
+    if (levels == 0) {
+        double *a = malloc(sizeof(double) * n), *d = malloc(sizeof(double) * n);
+        st = vwo_modwt_forward(x, n, lo, hi, L, boundary, a, d, bad_index);
+        double T = fixed;
+        if (st == VWO_OK && method != VWO_THR_FIXED) st = vwo_calc_threshold(d, n, vwo_noise_sigma(d, n), method, &T);
+        if (st == VWO_OK) {
+            vwo_threshold(d, n, T, soft);
+            vwo_modwt_inverse(a, d, n, lo, hi, L, boundary, 0, y);
+            if (thr_out) thr_out[0] = T;
+        }
+        free(a); free(d);
+        return st;
+    }
+    if (method == VWO_THR_FIXED) return VWO_ERR_ARG;
+    double *det = malloc(sizeof(double) * (size_t)n * levels), *app = malloc(sizeof(double) * n);
+    st = vwo_ml_decompose(x, n, lo, hi, L, boundary, levels, 1, det, app, bad_index);
+    if (st == VWO_OK) {
+        double sigma = vwo_noise_sigma(det, n);
+        for (int level = 1; level <= levels && st == VWO_OK; level++) {
+            double *dl = det + (size_t)(level - 1) * n;
+            double levelScale = sqrt((double)(1 << level));
+            double T = 0;
+            st = vwo_calc_threshold(dl, n, sigma / levelScale, method, &T);
+            vwo_threshold(dl, n, T, soft);
+            if (thr_out) thr_out[level - 1] = T;
+        }
+    }
+    if (st == VWO_OK) st = vwo_ml_reconstruct(det, app, n, lo, hi, L, wavelet_id, boundary, levels, 0xFFFFFFFFu, 0, y);
+    free(det); free(app);
+    return st;
+}
+
 /* --------------------------------------------------------------- A16 ---- */
 /* BatchSIMDMODWT.batchMODWTSoA single level  ext/extensions/modwt/BatchSIMDMODWT.java:64-274.
  * Haar uses the hard-coded 0.5/-0.5 taps (:86-140); L == 4 takes the "db4" branch (:145-206). */

@@ -317,3 +317,76 @@ def test_java_random_matches_reference_stream():
     r = O.JavaRandom(42)
     assert r.nextDouble() == 0.7275636800328681
     assert r.nextDouble() == 0.6832234717598454
+
+
+# ---- WaveletDenoiser restatement (core/denoising/WaveletDenoiser.java) ---------------------------
+def _np_sure(c, sigma):
+    """calculateSUREThreshold :441-472 restated independently (numpy sums: tolerance-level agreement)."""
+    a = np.sort(np.abs(c))
+    n = len(c)
+    risks = [(-n * sigma ** 2 + np.sum(np.where(np.abs(c) <= t, c * c, sigma ** 2 + (np.abs(c) - t) ** 2))) / n
+             for t in a]
+    best = a[int(np.argmin(risks))]
+    return min(best, sigma * math.sqrt(2 * math.log(n))), min(risks)
+
+
+def test_sure_threshold_restatement():
+    rng = np.random.default_rng(4)
+    for n in (5, 64, 300):
+        c = rng.standard_normal(n) * 0.7
+        c[: n // 10] *= 8  # a few large coefficients: the search has an interior minimum
+        sigma = O.noise_sigma(c)
+        t = O.calc_threshold(c, sigma, O.SURE)
+        t_np, r_np = _np_sure(c, sigma)
+        # the restatement's choice is a minimiser of the risk (argmin can differ only within rounding)
+        assert abs(O.sure_risk(c, t, sigma) - r_np) <= 1e-12 * max(1.0, abs(r_np)) or t == t_np
+        assert t <= sigma * math.sqrt(2 * math.log(n)) and t >= 0
+
+
+def test_minimax_and_universal_and_bayes_restatement():
+    # calculateMinimaxThreshold :497-509
+    assert O.calc_threshold(np.zeros(32), 1.0, O.MINIMAX) == 0.0
+    lg = math.log(64)
+    assert O.calc_threshold(np.zeros(64), 2.0, O.MINIMAX) == 2.0 * 0.3936 + 0.1829 * 2.0 * lg
+    lg = math.log(65)
+    assert O.calc_threshold(np.zeros(65), 2.0, O.MINIMAX) == 2.0 * (0.4745 + 0.1148 * lg)
+    assert O.calc_threshold(np.zeros(100), 1.5, O.UNIVERSAL) == 1.5 * math.sqrt(2.0 * math.log(100))
+    # calculateBayesThreshold :521-549 (sequential sums)
+    rng = np.random.default_rng(9)
+    c = rng.standard_normal(1000) * 2.0
+    sigma = 0.8
+    mean = 0.0
+    for v in c:
+        mean += v
+    mean /= len(c)
+    var = 0.0
+    for v in c:
+        var += (v - mean) * (v - mean)
+    var /= len(c)
+    assert O.calc_threshold(c, sigma, O.BAYES) == sigma * sigma / math.sqrt(max(0.0, var - sigma * sigma) + 1e-10)
+    with pytest.raises(O.OracleError):
+        O.calc_threshold(c, sigma, O.FIXED)
+
+
+def test_wavelet_denoise_restatement_properties():
+    # WaveletDenoiserTest / WaveletDenoiserBayesTest invariants on the restatement
+    w = Daubechies.DB4
+    lo, hi = w.lowPassDecomposition(), w.highPassDecomposition()
+    rng = np.random.default_rng(2)
+    n = 256
+    clean = np.sin(2 * np.pi * np.arange(n) / 32)
+    x = clean + 0.5 * rng.standard_normal(n)
+    for m in (O.UNIVERSAL, O.SURE, O.MINIMAX, O.BAYES):
+        for levels in (0, 3):
+            y, thr = O.wavelet_denoise(x, lo, hi, O.PERIODIC, levels, m)
+            assert y.shape == x.shape and np.all(np.isfinite(y)) and np.all(thr >= 0)
+            assert np.var(y - clean) <= np.var(x - clean) * 1.1, (m, levels)
+        # multi-level thresholds: level j uses sigma / sqrt(2^j) -> universal thresholds halve every 2 levels
+    y, thr = O.wavelet_denoise(x, lo, hi, O.PERIODIC, 4, O.UNIVERSAL)
+    np.testing.assert_allclose(thr[2] / thr[0], 0.5, rtol=1e-15)
+    # a zero threshold reconstructs the MODWT round trip
+    y0, _ = O.wavelet_denoise(x, lo, hi, O.PERIODIC, 0, O.FIXED, 0.0)
+    a, d = O.modwt_forward(x, lo, hi, O.PERIODIC)
+    assert np.array_equal(y0, O.modwt_inverse(a, d, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC))
+    with pytest.raises(O.OracleError):
+        O.wavelet_denoise(x, lo, hi, O.PERIODIC, 2, O.FIXED, 0.1)

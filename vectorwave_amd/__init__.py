@@ -6,6 +6,7 @@ include/vectorwave_amd.h).  This package is the host-side mirror of the referenc
   MODWTTransform, MultiLevelMODWTTransform, MODWTResult, MultiLevelMODWTResult,
   MutableMultiLevelMODWTResult, BoundaryMode                  (core/modwt, core/api)
   VectorWaveSwtAdapter                                        (core/swt)
+  WaveletDenoiser                                             (core/denoising)
   BatchMODWT, BatchStreamingMODWT                             (ext/extensions/modwt)
   Haar, Daubechies, Symlet, Coiflet                           (core/api wavelets)
 """
@@ -15,6 +16,7 @@ from .errors import (ErrorCode, InvalidArgumentException, InvalidSignalException
 from .modwt import (BoundaryMode, MODWTResult, MODWTTransform, MultiLevelMODWTResult, MultiLevelMODWTTransform,
                     MutableMultiLevelMODWTResult)
 from .swt import VectorWaveSwtAdapter
+from .denoise import ThresholdMethod, ThresholdType, WaveletDenoiser
 from .batch import BatchMODWT, BatchStreamingMODWT
 from .engine import Engine, max_levels, version
 
@@ -23,5 +25,6 @@ __all__ = [
     "ErrorCode", "InvalidArgumentException", "InvalidSignalException", "InvalidStateException",
     "WaveletTransformException", "BoundaryMode", "MODWTResult", "MODWTTransform", "MultiLevelMODWTResult",
     "MultiLevelMODWTTransform", "MutableMultiLevelMODWTResult", "VectorWaveSwtAdapter", "BatchMODWT",
+    "WaveletDenoiser", "ThresholdMethod", "ThresholdType",
     "BatchStreamingMODWT", "Engine", "max_levels", "version",
 ]

@@ -54,6 +54,8 @@ SIGNATURES = {
                                       c_void_p]),
     "vw_swt_denoise_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, _dp, _dp, c_int, c_int, c_int,
                                    c_int, c_double, c_int, c_uint, c_void_p, c_void_p]),
+    "vw_wavelet_denoise_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, _dp, _dp, c_int, c_int, c_int,
+                                       c_int, c_int, c_double, c_int, c_uint, c_void_p, c_void_p]),
     "vw_noise_sigma_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_uint, c_void_p]),
     "vw_threshold_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int, c_uint]),
     "vw_stream_create": (c_int, [c_void_p, _dp, _dp, c_int, c_int, c_int, POINTER(c_void_p)]),

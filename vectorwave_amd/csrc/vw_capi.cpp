@@ -594,7 +594,8 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
 template <typename T>
 static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int64_t B, int64_t N, const double* lo,
                               const double* hi, int L, int wid, int boundary, int J, unsigned detail_mask,
-                              int approx_zero, unsigned flags, T* y, bool single_level, const T* thr, int soft) {
+                              int approx_zero, unsigned flags, T* y, bool single_level, const T* thr, int soft,
+                              int64_t thr_ld = 0) {
   constexpr int V = vec_width<T>();
   const bool fma = flags & VW_FLAG_FMA;
   const int64_t nvec = (N + V - 1) / V;
@@ -655,7 +656,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     a.hlpad_a = hlpad; a.hlpad_d = hlpad; a.region_d = (int)region;
     a.vec_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
     a.unrolled = a.vec_io && fit;
-    a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.soft = soft; a.taps = L;
+    a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.thr_ld = thr_ld; a.soft = soft; a.taps = L;
     a.rev = getenv("VW_INV_REV") ? atoi(getenv("VW_INV_REV")) : 0;
     copy_taps(a.lo, lo, L);
     copy_taps(a.hi, hi, L);
@@ -689,7 +690,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       a.use_d = a.lv.use_d;
       a.out_a = (j == 1) ? y : tmp[j & 1];
       a.B = B; a.N = (int)N; a.tile = tile; a.hlpad = hp; a.hlpad_d = hp; a.region_d = (int)reg;
-      a.pair = pair; a.thr = thr; a.soft = soft; a.taps = L;
+      a.pair = pair; a.thr = thr ? thr + (size_t)(j - 1) * (size_t)thr_ld : nullptr; a.soft = soft; a.taps = L;
       a.vec_io = (N % V == 0) && aligned16(a.out_a) && aligned16(a.src_a) && aligned16(a.src_d);
       copy_taps(a.lo, lo, L);
       copy_taps(a.hi, hi, L);
@@ -1006,6 +1007,112 @@ extern "C" vw_status vw_swt_denoise_f64(vw_ctx* c, const double* x, int64_t B, i
     return ok();
   }
   VW_TRY(denoise_device(c, x, B, N, ldx, lo, hi, L, wid, boundary, J, threshold, soft, flags, y, thresholds_out));
+  if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}
+
+// ------------------------------------------------------------------------------------------------
+// WaveletDenoiser (core/denoising/WaveletDenoiser.java): forward (single-level MODWTTransform for
+// denoise()/denoiseFixed(), MultiLevelMODWTTransform for denoiseMultiLevel()), sigma = MAD of d_1,
+// one threshold per (level, signal) by the method (vw_sigma.h), inverse with the per-level threshold
+// fused into the detail staging.
+static vw_status wavelet_denoise_device(vw_ctx* c, const double* x, int64_t B, int64_t N, int64_t ldx,
+                                        const double* lo, const double* hi, int L, int wid, int boundary, int levels,
+                                        int method, double fixed, int soft, unsigned flags, double* y,
+                                        double* thr_out) {
+  const int J = levels > 0 ? levels : 1;
+  const size_t plane = (size_t)B * (size_t)N;
+  const size_t coef_bytes = align_up(((size_t)J + 1) * plane * sizeof(double), 256);
+  const size_t bytes = coef_bytes + align_up((size_t)B * 8, 256) + align_up((size_t)J * B * 8, 256);
+  if (bytes > c->ws2_bytes) {
+    if (c->ws2) {
+      hipStreamSynchronize(c->stream);
+      hipFree(c->ws2);
+      c->ws2 = nullptr;
+      c->ws2_bytes = 0;
+    }
+    VW_HIP(hipMalloc(&c->ws2, bytes));
+    c->ws2_bytes = bytes;
+  }
+  double* det = reinterpret_cast<double*>(c->ws2);
+  double* app = det + (size_t)J * plane;
+  double* sig = reinterpret_cast<double*>(reinterpret_cast<char*>(c->ws2) + coef_bytes);
+  double* thr = reinterpret_cast<double*>(reinterpret_cast<char*>(sig) + align_up((size_t)B * 8, 256));
+  const unsigned fl = flags & ~VW_FLAG_SYNC;
+  vw_status st = levels > 0 ? forward_impl<double>(c, x, B, N, ldx, lo, hi, L, boundary, J, fl, det, app, false, -1,
+                                                   nullptr, false)
+                            : forward_impl<double>(c, x, B, N, ldx, lo, hi, L, boundary, 1, fl & ~VW_FLAG_FFT_SWITCH,
+                                                   det, app, true, -1, nullptr, false);
+  if (st != VW_OK) return st;
+  hipError_t e = hipSuccess;
+  if (method == kThrFixed) {
+    std::vector<double> h((size_t)B, fixed);
+    e = hipMemcpyAsync(thr, h.data(), (size_t)B * sizeof(double), hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  } else {
+    DenoiseConsts k;
+    memset(&k, 0, sizeof(k));
+    for (int j = 1; j <= J; ++j) k.level_scale[j - 1] = levels > 0 ? std::sqrt((double)(1 << j)) : 1.0;
+    k.univ_c = std::sqrt(2.0 * std::log((double)N));
+    k.log_n = std::log((double)N);
+    k.method = method;
+    k.n = (int)N;
+    {
+      LaunchTimer lt(c, "sigma");
+      e = launch_noise_sigma(det, N, B, (int)N, 0.0, sig, nullptr, c->stream);
+    }
+    if (e == hipSuccess) {
+      LaunchTimer lt(c, "threshold");
+      e = launch_level_threshold(det, (long long)plane, sig, k, B, J, thr, c->stream);
+    }
+  }
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "threshold stage failed: %s", hipGetErrorString(e));
+  if (levels > 0)
+    st = inverse_impl<double>(c, det, app, B, N, lo, hi, L, wid, boundary, J, ~0u, 0, fl, y, false, thr, soft, B);
+  else
+    st = inverse_impl<double>(c, det, app, B, N, lo, hi, L, VW_WID_OTHER, boundary, 1, 1u, 0, fl, y, true, thr, soft);
+  if (st == VW_OK && thr_out) {
+    e = hipMemcpyAsync(thr_out, thr, (size_t)J * B * sizeof(double), hipMemcpyDeviceToDevice, c->stream);
+    if (e != hipSuccess) st = fail(VW_ERR_DEVICE, "copy failed");
+  }
+  return st;
+}
+
+extern "C" vw_status vw_wavelet_denoise_f64(vw_ctx* c, const double* x, int64_t B, int64_t N, int64_t ldx,
+                                            const double* lo, const double* hi, int L, int wid, int boundary,
+                                            int levels, int method, double fixed_threshold, int soft, unsigned flags,
+                                            double* y, double* thresholds_out) {
+  VW_TRY(check_common(c, x, y, lo, hi, B, N, L, boundary));
+  if (ldx < N) return fail(VW_ERR_ARG, "ldx < N");
+  if (method < kThrUniversal || method > kThrFixed) return fail(VW_ERR_ARG, "Unknown threshold selection method");
+  if (levels < 0) return fail(VW_ERR_LEVEL, "Invalid number of decomposition levels: %d", levels);
+  if (levels > 0) {
+    // calculateThreshold (:415-424): FIXED needs an explicit threshold (denoiseFixed is single-level)
+    if (method == kThrFixed) return fail(VW_ERR_ARG, "Fixed threshold method requires explicit threshold value");
+    VW_TRY(check_levels(N, L, levels, flags));
+    if (vw_upsampled_length(L, levels) > N && boundary != VW_PERIODIC)
+      return fail(VW_ERR_TOO_LARGE, "Upsampled reconstruction filter length exceeds signal length");
+  }
+  if (method == kThrSure && N > kSureMaxN)
+    return fail(VW_ERR_UNSUPPORTED, "SURE threshold on device supports N <= %d (got %lld)", kSureMaxN, (long long)N);
+  const int J = levels > 0 ? levels : 1;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (flags & VW_FLAG_HOST_MEMORY) {
+    Staging s(c);
+    double *dx, *dy, *dt = nullptr;
+    VW_TRY(s.in(x, (size_t)B * ldx, &dx));
+    VW_TRY(s.in<double>(nullptr, (size_t)B * N, &dy));
+    if (thresholds_out) VW_TRY(s.in<double>(nullptr, (size_t)J * B, &dt));
+    VW_TRY(wavelet_denoise_device(c, dx, B, N, ldx, lo, hi, L, wid, boundary, levels, method, fixed_threshold, soft,
+                                  flags & ~VW_FLAG_HOST_MEMORY, dy, dt));
+    VW_TRY(s.out(y, dy, (size_t)B * N));
+    if (thresholds_out) VW_TRY(s.out(thresholds_out, dt, (size_t)J * B));
+    VW_HIP(hipStreamSynchronize(c->stream));
+    return ok();
+  }
+  VW_TRY(wavelet_denoise_device(c, x, B, N, ldx, lo, hi, L, wid, boundary, levels, method, fixed_threshold, soft, flags,
+                                y, thresholds_out));
   if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
   return ok();
 }

@@ -385,7 +385,8 @@ __device__ __forceinline__ T threshold_t(T c, T thr, int soft) {
   const T av = c < T(0) ? -c : c;
   if (soft) {
     // Math.signum(c) * (|c| - T): c != 0 here, and a product with +-1 is a sign flip, i.e. copysign
-    if (av > thr) return __builtin_copysign(av - thr, c);
+    // (c == 0 passes only for a negative threshold: signum(+-0) * x = +-0 * x)
+    if (av > thr) return c == T(0) ? c * (av - thr) : __builtin_copysign(av - thr, c);
     return T(0);
   }
   return av <= thr ? T(0) : c;
@@ -811,7 +812,8 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_fused(const InvA
   const int N = p.N;
   const int nvec = (N + V - 1) / V;
   const bool vec_ok = (L > 0) || p.vec_io != 0;
-  const T thr_b = p.thr ? p.thr[b] : T(0);
+  // threshold of level j (denoise): thr[(j-1)*thr_ld + b]; thr_ld = 0 -> one threshold for every level
+  auto thr_of = [&](int j) { return p.thr ? p.thr[(size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b] : T(0); };
   const size_t plane = (size_t)p.B * (size_t)N;
 
   T reg[NV][V];
@@ -823,7 +825,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_fused(const InvA
   wait_vmem();
   regs_to_level<T, L, NV>(A, reg, nvec, N, p.lv[p.J - 1], 0, (const T*)nullptr, p.approx_zero != 0);
   regs_to_level<T, L, NV>(D, dnext, nvec, N, p.lv[p.J - 1], 0, (const T*)nullptr, p.lv[p.J - 1].use_d == 0, p.thr,
-                          thr_b, p.soft);
+                          thr_of(p.J), p.soft);
 
   for (int j = p.J; j >= 1; --j) {
     const LevelDesc lv = p.lv[j - 1];
@@ -850,7 +852,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_fused(const InvA
       lds_barrier();  // all reads of A and D done
       regs_to_level<T, L, NV>(A, reg, nvec, N, ln, 0, (const T*)nullptr);
       wait_vmem();  // the d_{j-1} prefetch
-      regs_to_level<T, L, NV>(D, dnext, nvec, N, ln, 0, (const T*)nullptr, ln.use_d == 0, p.thr, thr_b, p.soft);
+      regs_to_level<T, L, NV>(D, dnext, nvec, N, ln, 0, (const T*)nullptr, ln.use_d == 0, p.thr, thr_of(j - 1), p.soft);
     }
   }
 }
@@ -870,7 +872,8 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_db(const InvArgs
   const int N = p.N;
   const int nvec = (N + V - 1) / V;
   const bool vec_ok = (L > 0) || p.vec_io != 0;
-  const T thr_b = p.thr ? p.thr[b] : T(0);
+  // threshold of level j (denoise): thr[(j-1)*thr_ld + b]; thr_ld = 0 -> one threshold for every level
+  auto thr_of = [&](int j) { return p.thr ? p.thr[(size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b] : T(0); };
   const size_t plane = (size_t)p.B * (size_t)N;
 
   T acc[NV][V];
@@ -885,7 +888,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_db(const InvArgs
     const LevelDesc lv = p.lv[j - 1];
     lds_barrier();  // X = a_j + halo; every read of Y (previous level) done
     wait_vmem();    // the d_j prefetch (the only global ops in flight)
-    regs_to_level<T, L, NV>(Y, dreg, nvec, N, lv, 0, (const T*)nullptr, lv.use_d == 0, p.thr, thr_b, p.soft);
+    regs_to_level<T, L, NV>(Y, dreg, nvec, N, lv, 0, (const T*)nullptr, lv.use_d == 0, p.thr, thr_of(j), p.soft);
     if (j > 1)
       load_row_regs<T, NV>(dreg, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, vec_ok,
                            p.lv[j - 2].use_d == 0);
@@ -909,7 +912,8 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_seq(const InvArg
   const int N = p.N;
   const int nvec = (N + V - 1) / V;
   const bool vec_ok = (L > 0) || p.vec_io != 0;
-  const T thr_b = p.thr ? p.thr[b] : T(0);
+  // threshold of level j (denoise): thr[(j-1)*thr_ld + b]; thr_ld = 0 -> one threshold for every level
+  auto thr_of = [&](int j) { return p.thr ? p.thr[(size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b] : T(0); };
   const size_t plane = (size_t)p.B * (size_t)N;
 
   T acc[NV][V];
@@ -927,7 +931,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_seq(const InvArg
     inv_row<T, L, FMA, NV>(R, nvec, lv.s, lv.dir_a, lv.off_a, p.lo, p.taps, acc);
     lds_barrier();  // every approximation-branch read done
     wait_vmem();    // the d_j prefetch
-    regs_to_level<T, L, NV>(R, dreg, nvec, N, lv, 0, (const T*)nullptr, lv.use_d == 0, p.thr, thr_b, p.soft);
+    regs_to_level<T, L, NV>(R, dreg, nvec, N, lv, 0, (const T*)nullptr, lv.use_d == 0, p.thr, thr_of(j), p.soft);
     if (j > 1)
       load_row_regs<T, NV>(dreg, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, vec_ok,
                            p.lv[j - 2].use_d == 0);
@@ -1036,7 +1040,7 @@ __global__ void __launch_bounds__(256) k_inverse_level(const LevelArgs<T> p) {
   const int cnt = min(p.tile, N - ts);
   const int nv = (cnt + V - 1) / V;
   const LevelDesc lv = p.lv;
-  const T thr_b = p.thr ? p.thr[b] : T(0);
+  const T thr_b = p.thr ? p.thr[b] : T(0);  // this launch is one level: the host offsets thr
   const int span = nv * V;
   tile_to_lds(A, p.src_a + b * (size_t)N, N, ts, -lv.hl, span + lv.hr, lv.mode, 0, (const T*)nullptr, 0,
               (const T*)nullptr, T(0), 0, p.src_a == nullptr, p.vec_io != 0);

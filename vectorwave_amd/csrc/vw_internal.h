@@ -82,7 +82,8 @@ struct InvArgs {
   int db;               // sequential sum: 1 = two LDS buffers (k_inverse_db), 0 = one (k_inverse_seq)
   int approx_zero;
   int rev;              // 1: workgroup g owns signal B-1-g
-  const T* thr;         // per-signal threshold [B] (nullptr = no thresholding)
+  const T* thr;         // thresholds [J][thr_ld] (nullptr = no thresholding)
+  long long thr_ld;     // level stride of thr (0: one threshold per signal for every level)
   int soft;
   int taps;
   T lo[kMaxTaps];
@@ -118,6 +119,18 @@ struct LevelArgs {
   LevelDesc lv;
 };
 
+// WaveletDenoiser threshold methods (core/denoising/WaveletDenoiser.java:588-622) and the per-launch
+// constants of the threshold kernels (vw_sigma.h).
+enum ThrMethod { kThrUniversal = 0, kThrSure = 1, kThrMinimax = 2, kThrBayes = 3, kThrFixed = 4 };
+constexpr int kSureMaxN = 16384;  // SURE on device: the sorted row lives in LDS
+struct DenoiseConsts {
+  double level_scale[kMaxLevels];  // Math.sqrt(1 << level) (denoiseMultiLevel, :225), 1 for denoise()
+  double univ_c;                   // Math.sqrt(2.0 * Math.log(n))
+  double log_n;                    // Math.log(n)
+  int method;
+  int n;
+};
+
 // Launchers (vw_kernels.hip).  Return hipSuccess or the launch error.
 template <typename T>
 hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
@@ -137,6 +150,8 @@ template <typename T>
 hipError_t launch_history_update(const T* level_in, long long ld_in, const T* old_hist, T* new_hist,
                                  long long B, int n, int hist_len, hipStream_t st);
 
+hipError_t launch_level_threshold(const double* coeffs, long long level_stride, const double* sigma,
+                                  const DenoiseConsts& k, long long B, int levels, double* thr, hipStream_t st);
 hipError_t launch_noise_sigma(const double* coeffs, long long ld, long long B, int N, double scale_c,
                               double* sigma_out, double* thr_out, hipStream_t st);
 template <typename T>

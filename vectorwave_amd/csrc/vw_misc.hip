@@ -53,6 +53,30 @@ hipError_t launch_noise_sigma(const double* coeffs, long long ld, long long B, i
   return hipGetLastError();
 }
 
+// WaveletDenoiser thresholds, one per (level, signal): SURE by the sort + exact-tie kernel, the others
+// by k_level_threshold.
+hipError_t launch_level_threshold(const double* coeffs, long long level_stride, const double* sigma,
+                                  const DenoiseConsts& k, long long B, int levels, double* thr, hipStream_t st) {
+  if (B <= 0 || levels <= 0) return hipSuccess;
+  const dim3 grid((unsigned)B, (unsigned)levels);
+  if (k.method == kThrSure) {
+    int npow2 = 1;
+    while (npow2 < k.n) npow2 <<= 1;
+    const int lds = npow2 * (int)sizeof(unsigned long long);
+    static int configured = 64 * 1024;  // (this kernel also has static LDS: raise the limit to what it asks)
+    if (lds > configured) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_sure_threshold),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+      if (e != hipSuccess) return e;
+      configured = lds;
+    }
+    hipLaunchKernelGGL(k_sure_threshold, grid, dim3(kSureThreads), lds, st, coeffs, level_stride, sigma, k, B, thr);
+  } else {
+    hipLaunchKernelGGL(k_level_threshold, grid, dim3(64), 0, st, coeffs, level_stride, sigma, k, B, thr);
+  }
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_threshold(T* c, long long B, long long N, const T* thr, int soft, hipStream_t st) {
   const long long total = B * N;

@@ -280,4 +280,208 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
 }
 
 
+
+// ---------------------------------------------------------------------------------------------
+// WaveletDenoiser thresholds (core/denoising/WaveletDenoiser.java:394-549), one per (level, signal):
+// grid (B, levels).  sigma[b] is the MAD estimate of d_1 (k_noise_sigma); level j uses
+// sigma / Math.sqrt(1 << j) (:225; 1 for the single-level denoise).  Host-side constants (the logs,
+// square roots) come from the host libm, as in the C restatement.
+//
+// UNIVERSAL / MINIMAX: closed forms.  BAYES: the reference's sequential mean and variance sums in
+// coefficient order, by one lane (bit-identical; rows are independent, so many waves run at once).
+__global__ void __launch_bounds__(64) k_level_threshold(const double* __restrict__ coeffs, long long level_stride,
+                                                        const double* __restrict__ sigma, const DenoiseConsts k,
+                                                        long long B, double* __restrict__ thr) {
+  if (threadIdx.x != 0) return;
+  const long long b = blockIdx.x;
+  const int lev = blockIdx.y;
+  const int n = k.n;
+  const double sig = sigma[b] / k.level_scale[lev];
+  double T = 0.0;
+  if (k.method == kThrUniversal) {
+    T = sig * k.univ_c;
+  } else if (k.method == kThrMinimax) {  // :497-509
+    if (n <= 32) T = 0;
+    else if (n <= 64) T = sig * 0.3936 + 0.1829 * sig * k.log_n;
+    else T = sig * (0.4745 + 0.1148 * k.log_n);
+  } else if (k.method == kThrBayes) {  // :521-549
+    const double* c = coeffs + (size_t)lev * (size_t)level_stride + (size_t)b * (size_t)n;
+    const double sigma2 = sig * sig;
+    double mean = 0.0;
+    for (int i = 0; i < n; ++i) mean += c[i];
+    mean /= n;
+    double variance = 0.0;
+    for (int i = 0; i < n; ++i) {
+      const double diff = c[i] - mean;
+      variance += diff * diff;
+    }
+    variance /= n;
+    const double sigmaX2 = variance - sigma2 > 0.0 ? variance - sigma2 : 0.0;  // Math.max(0.0, .)
+    const double sigmaX = __builtin_sqrt(sigmaX2 + 1e-10);                   // BAYES_EPSILON :62
+    T = sigma2 / sigmaX;
+  }
+  thr[(size_t)lev * (size_t)B + (size_t)b] = T;
+}
+
+// SURE (calculateSUREThreshold :441-472 + calculateSURERisk :477-492).  The reference tries every
+// sorted |c_k| as the threshold and evaluates the risk in O(n) each (O(n^2) per row), keeping the
+// first minimum.  Here, one workgroup per (signal, level):
+//   1. |c| bit patterns sorted in LDS (bitonic; non-negative doubles order as unsigned integers);
+//   2. the risk of every distinct t = a_k from prefix sums (one pass, O(n)):
+//        n * risk(t) = -n s^2 + sum_{a<=t} a^2 + sum_{a>t} (s^2 + (a - t)^2)
+//      (ties share t and the same risk, so only the last index of each run is scored);
+//   3. this approximation differs from the reference's sequential sum by at most a few n*eps*(s^2 +
+//      max a^2) (both sides' rounding); every t within kSureTol of that bound of the minimum is a
+//      candidate.  One candidate decides the threshold by itself; otherwise each candidate's risk is
+//      re-evaluated exactly as the reference does (sequential sum in coefficient order, one lane per
+//      candidate) and the smallest risk with the smallest t wins -- the reference's strict-< scan.
+//   4. the result is capped at the universal threshold (:466-469).
+// The threshold is therefore the reference's value bit for bit.  n <= kSureMaxN (LDS: the sorted keys).
+constexpr int kSureThreads = 1024;
+constexpr int kSureMaxChunks = kSureMaxN / kSureThreads;
+
+__device__ __forceinline__ double sure_exact_risk(const double* __restrict__ c, int n, double t, double s2) {
+  double risk = -n * s2;
+  for (int i = 0; i < n; ++i) {
+    const double x = c[i];
+    const double a = __builtin_fabs(x);
+    if (a <= t) risk += x * x;
+    else risk += s2 + (a - t) * (a - t);
+  }
+  return risk / n;
+}
+
+// inclusive block scan of (x, y) over 1024 threads; returns the block totals
+__device__ __forceinline__ void block_scan2(double& x, double& y, double* wx, double* wy, double* tx, double* ty) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const double px = __shfl_up(x, o, 64), py = __shfl_up(y, o, 64);
+    if (lane >= o) { x += px; y += py; }
+  }
+  __syncthreads();  // wx / wy free
+  if (lane == 63) { wx[wv] = x; wy[wv] = y; }
+  __syncthreads();
+  double bx = 0.0, by = 0.0, sx = 0.0, sy = 0.0;
+  for (int q = 0; q < kSureThreads / 64; ++q) {
+    if (q < wv) { bx += wx[q]; by += wy[q]; }
+    sx += wx[q];
+    sy += wy[q];
+  }
+  x += bx;
+  y += by;
+  *tx = sx;
+  *ty = sy;
+}
+
+__global__ void __launch_bounds__(kSureThreads) k_sure_threshold(const double* __restrict__ coeffs, long long level_stride,
+                                                                 const double* __restrict__ sigma, const DenoiseConsts k,
+                                                                 long long B, double* __restrict__ thr) {
+  extern __shared__ unsigned long long key[];
+  __shared__ double wx[kSureThreads / 64], wy[kSureThreads / 64];
+  __shared__ double red[kSureThreads / 64];
+  __shared__ int ired[kSureThreads / 64];
+  const int tid = threadIdx.x;
+  const long long b = blockIdx.x;
+  const int lev = blockIdx.y;
+  const int n = k.n;
+  const double* c = coeffs + (size_t)lev * (size_t)level_stride + (size_t)b * (size_t)n;
+  const double sig = sigma[b] / k.level_scale[lev];
+  const double s2 = sig * sig;
+  int npow2 = 1;
+  while (npow2 < n) npow2 <<= 1;
+  for (int i = tid; i < npow2; i += kSureThreads) key[i] = i < n ? abs_bits(c[i]) : 0x7FF0000000000000ull;
+  __syncthreads();
+  for (int size = 2; size <= npow2; size <<= 1) {  // bitonic sort, ascending
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < npow2 / 2; i += kSureThreads) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const unsigned long long x = key[lo], y = key[hi];
+        if ((x > y) == ((lo & size) == 0)) { key[lo] = y; key[hi] = x; }
+      }
+      __syncthreads();
+    }
+  }
+  auto val = [&](int i) { return __longlong_as_double((long long)key[i]); };
+  // totals
+  double s1 = 0.0, sq = 0.0;
+  for (int i = tid; i < n; i += kSureThreads) { const double a = val(i); s1 += a; sq += a * a; }
+  double S1, S2;
+  {
+    double x = s1, y = sq;
+    block_scan2(x, y, wx, wy, &S1, &S2);
+  }
+  const double amax = val(n - 1);
+  const double tol = 32.0 * n * 2.220446049250313e-16 * (s2 + amax * amax);
+  // approximate risk of every run's last index
+  const int nch = (n + kSureThreads - 1) / kSureThreads;
+  double risk[kSureMaxChunks];
+  double c1 = 0.0, c2 = 0.0;
+#pragma unroll
+  for (int ch = 0; ch < kSureMaxChunks; ++ch) {
+    risk[ch] = __builtin_inf();
+    if (ch < nch) {
+      const int kk = ch * kSureThreads + tid;
+      const double a = kk < n ? val(kk) : 0.0;
+      double p1 = a, p2 = a * a, t1, t2;
+      block_scan2(p1, p2, wx, wy, &t1, &t2);
+      p1 += c1;
+      p2 += c2;
+      c1 += t1;
+      c2 += t2;
+      if (kk < n && (kk == n - 1 || key[kk + 1] != key[kk])) {
+        const double up = (double)(n - kk - 1);
+        const double x = -n * s2 + p2 + up * s2 + (S2 - p2) - 2.0 * a * (S1 - p1) + up * a * a;
+        risk[ch] = x / n;
+      }
+    }
+  }
+  // minimum approximate risk
+  double m = __builtin_inf();
+#pragma unroll
+  for (int ch = 0; ch < kSureMaxChunks; ++ch) m = risk[ch] < m ? risk[ch] : m;
+  m = block_minmax(m, false, red);
+  // candidates
+  int cnt = 0, first = 0x7FFFFFFF;
+#pragma unroll
+  for (int ch = 0; ch < kSureMaxChunks; ++ch)
+    if (risk[ch] <= m + tol && risk[ch] < __builtin_inf()) { ++cnt; first = min(first, ch * kSureThreads + tid); }
+  // count and (for a single candidate) its index
+  int total = cnt;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) total += __shfl_xor(total, o, 64);
+  __syncthreads();
+  if ((tid & 63) == 0) ired[tid >> 6] = total;
+  __syncthreads();
+  total = 0;
+  for (int q = 0; q < kSureThreads / 64; ++q) total += ired[q];
+  int best_k = -1;
+  if (total == 1) {
+    best_k = (int)block_minmax((double)first, false, red);
+  } else if (total > 1) {
+    // exact risks of the candidates (a lane per candidate, chunk by chunk), then (risk, index) minimum
+    double em = __builtin_inf();
+    int ek = 0x7FFFFFFF;
+#pragma unroll
+    for (int ch = 0; ch < kSureMaxChunks; ++ch) {
+      if (risk[ch] <= m + tol && risk[ch] < __builtin_inf()) {
+        const int kk = ch * kSureThreads + tid;
+        const double r = sure_exact_risk(c, n, val(kk), s2);
+        if (r < em) { em = r; ek = kk; }  // kk ascends with ch: ties keep the smaller index
+      }
+    }
+    const double emin = block_minmax(em, false, red);
+    const double kd = em == emin ? (double)ek : 1e300;
+    const double kmin = block_minmax(kd, false, red);
+    best_k = kmin < 1e300 ? (int)kmin : -1;
+  }
+  if (tid == 0) {
+    double best = best_k >= 0 ? val(best_k) : 0.0;
+    const double universal = sig * k.univ_c;
+    if (best > universal) best = universal;
+    thr[(size_t)lev * (size_t)B + (size_t)b] = best;
+  }
+}
+
 }  // namespace vw

@@ -183,6 +183,19 @@ class Engine:
                                            self._flags(flags, dev), self._ptr(y, dev), self._ptr(thr, dev)))
         return (y, thr) if want_thresholds else y
 
+    def wavelet_denoise(self, x, lo, hi, wavelet_id: int, boundary: int, levels: int, method: int, fixed: float,
+                        soft: bool, flags: int, want_thresholds: bool = False):
+        """vw_wavelet_denoise_f64 (WaveletDenoiser); thresholds [max(levels,1), B]."""
+        xa, dev, xp, _ = self._prep(x, np.float64)
+        one = xa.ndim == 1
+        B, N = (1, xa.shape[0]) if one else xa.shape
+        y = self._empty(xa, dev, xa.shape)
+        thr = self._empty(xa, dev, (max(levels, 1), B)) if want_thresholds else None
+        _check(self.lib.vw_wavelet_denoise_f64(self.ctx, xp, B, N, N, nat.taps_array(lo), nat.taps_array(hi), len(lo),
+                                               wavelet_id, boundary, levels, method, float(fixed), 1 if soft else 0,
+                                               self._flags(flags, dev), self._ptr(y, dev), self._ptr(thr, dev)))
+        return (y, thr) if want_thresholds else y
+
     def noise_sigma(self, coeffs):
         ca, dev, cp, _ = self._prep(coeffs, np.float64)
         one = ca.ndim == 1

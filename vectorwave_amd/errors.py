@@ -18,6 +18,8 @@ class ErrorCode(enum.Enum):
     VAL_EMPTY = ("VAL_006", "Empty input")
     CFG_UNSUPPORTED_BOUNDARY_MODE = ("CFG_003", "Unsupported boundary mode")
     CFG_INVALID_DECOMPOSITION_LEVEL = ("CFG_004", "Invalid decomposition level")
+    CFG_UNSUPPORTED_OPERATION = ("CFG_001", "Unsupported operation")
+    VAL_NULL_ARGUMENT = ("VAL_001", "Null argument")
     STATE_INVALID = ("STATE_001", "Invalid state")
 
     @property
