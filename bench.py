@@ -94,6 +94,8 @@ def main():
     # (distinct data per rank, generated on device from the global row index), no exchange
     from vectorwave_amd.shard import shard_rows
     start, Bg = shard_rows(world * Bg, world, rank)
+    # all work on one dedicated (non-default) stream: the engine binds to it, torch allocations order on it
+    torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     x = torch.empty((Bg, N), dtype=tdt, device=dev)
     eng.fill_uniform(x, 42, offset=start * N)
     det = torch.empty((J, Bg, N), dtype=tdt, device=dev)

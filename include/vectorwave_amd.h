@@ -26,6 +26,9 @@
  *   vw_swt_denoise_*        VectorWaveSwtAdapter.denoise  core/swt/VectorWaveSwtAdapter.java:532-562
  *   vw_noise_sigma_*        VectorWaveSwtAdapter.estimateNoiseSigma  core/swt/VectorWaveSwtAdapter.java:627-645
  *   vw_threshold_*          MutableMultiLevelMODWTResult.applyThreshold  core/modwt/MutableMultiLevelMODWTResult.java:83-114
+ *   vw_wavelet_denoise_*    WaveletDenoiser.denoise / denoiseMultiLevel / denoiseFixed
+ *                             core/denoising/WaveletDenoiser.java:111-549
+ *   vw_transpose_*          BatchSIMDMODWT.convertToSoA / convertFromSoA  ext/extensions/modwt/BatchSIMDMODWT.java:282-308
  *   vw_stream_*             BatchStreamingMODWT  ext/extensions/modwt/BatchStreamingMODWT.java:55-275
  *   vw_max_levels           MultiLevelMODWTTransform.getMaximumLevels  core/modwt/MultiLevelMODWTTransform.java:455-501, :693-695
  *   status codes            core/exception/ErrorCode.java:24-118 (see the table below)
@@ -125,6 +128,8 @@ VW_API vw_status vw_ctx_create(int device, vw_ctx **out);
 VW_API vw_status vw_ctx_destroy(vw_ctx *ctx);
 /* Use an external hipStream_t (e.g. torch.cuda.current_stream().cuda_stream); NULL = own stream. */
 VW_API vw_status vw_ctx_set_stream(vw_ctx *ctx, void *hip_stream);
+/* Enqueue on the device's null (legacy default) stream, e.g. torch's default stream (handle 0). */
+VW_API vw_status vw_ctx_use_null_stream(vw_ctx *ctx);
 VW_API void *vw_ctx_get_stream(vw_ctx *ctx);
 VW_API vw_status vw_ctx_synchronize(vw_ctx *ctx);
 VW_API int vw_ctx_device(vw_ctx *ctx);
@@ -179,6 +184,15 @@ VW_API vw_status vw_swt_denoise_f64(vw_ctx *ctx, const double *x, int64_t B, int
                                     const double *lo, const double *hi, int L, int wavelet_id,
                                     int boundary, int J, double threshold, int soft, unsigned flags,
                                     double *y, double *thresholds_out);
+/* ---- AoS <-> SoA layout (BatchSIMDMODWT.convertToSoA / convertFromSoA) -- */
+/* out[c][r] = in[r][c] for a rows x cols row-major matrix (out of place).  AoS double[B][N] -> the
+ * facade's SoA double[N*B] (index t*B + b): rows = B, cols = N; back: rows = N, cols = B.
+ * ext/extensions/modwt/BatchSIMDMODWT.java:282-308. */
+VW_API vw_status vw_transpose_f64(vw_ctx *ctx, const double *in, int64_t rows, int64_t cols, unsigned flags,
+                                  double *out);
+VW_API vw_status vw_transpose_f32(vw_ctx *ctx, const float *in, int64_t rows, int64_t cols, unsigned flags,
+                                  float *out);
+
 /* ---- WaveletDenoiser ---------------------------------------------------- */
 /* Replaces com.morphiqlabs.wavelet.denoising.WaveletDenoiser (core/denoising/WaveletDenoiser.java):
  *   levels == 0, method != FIXED : denoise(signal, method, type)            :124-143

@@ -411,3 +411,36 @@ def test_headline_device_resident_properties(engine):
         d, a = O.decompose(x[b].cpu().numpy(), *lohi(w), O.PERIODIC, J)
         exact(det[:, b, :].cpu().numpy(), d)
         exact(app[b].cpu().numpy(), a)
+
+
+# ---- SoA facade (BatchSIMDMODWT) -----------------------------------------------------------------------
+@pytest.mark.parametrize("B,n", [(3, 1000), (130, 67), (64, 64), (1, 5)])
+def test_soa_layout_round_trip(engine, B, n):
+    import torch
+    x = signals(B, n, 3)
+    soa = vw.BatchSIMDMODWT.convertToSoA(x)
+    exact(soa, x.T.reshape(-1))                              # convertToSoA :282-292: index t*B + b
+    exact(vw.BatchSIMDMODWT.convertFromSoA(soa, B, n), x)     # convertFromSoA :299-308
+    xd = torch.tensor(x, device="cuda")
+    sd = vw.BatchSIMDMODWT.convertToSoA(xd)
+    assert sd.is_cuda
+    exact(sd.cpu().numpy(), x.T.reshape(-1))
+
+
+@pytest.mark.parametrize("w", [H, Daubechies.DB2, Daubechies.DB4, Symlet.SYM8], ids=lambda w: w.name())
+def test_soa_single_and_multilevel_match_restatement(engine, w):
+    B, n = 5, 256
+    x = signals(B, n, 21)
+    soa = x.T.reshape(-1).copy()
+    sa, sd = vw.BatchSIMDMODWT.batchMODWTSoA(soa, w, B, n)
+    for b in range(B):
+        ra, rd = O.batch_single(x[b], *lohi(w), w is H)
+        exact(sa.reshape(n, B)[:, b], ra)
+        exact(sd.reshape(n, B)[:, b], rd)
+    J = 4
+    sdet, sapp = vw.BatchSIMDMODWT.batchMultiLevelMODWTSoA(soa, w, B, n, J)
+    assert sdet.shape == (J, n * B)
+    for b in range(B):
+        d, a = O.decompose(x[b], *lohi(w), O.PERIODIC, J, core=False)
+        exact(sdet.reshape(J, n, B)[:, :, b], d)
+        exact(sapp.reshape(n, B)[:, b], a)

@@ -17,7 +17,7 @@ from .modwt import (BoundaryMode, MODWTResult, MODWTTransform, MultiLevelMODWTRe
                     MutableMultiLevelMODWTResult)
 from .swt import VectorWaveSwtAdapter
 from .denoise import ThresholdMethod, ThresholdType, WaveletDenoiser
-from .batch import BatchMODWT, BatchStreamingMODWT
+from .batch import BatchMODWT, BatchSIMDMODWT, BatchStreamingMODWT
 from .engine import Engine, max_levels, version
 
 __all__ = [
@@ -25,6 +25,6 @@ __all__ = [
     "ErrorCode", "InvalidArgumentException", "InvalidSignalException", "InvalidStateException",
     "WaveletTransformException", "BoundaryMode", "MODWTResult", "MODWTTransform", "MultiLevelMODWTResult",
     "MultiLevelMODWTTransform", "MutableMultiLevelMODWTResult", "VectorWaveSwtAdapter", "BatchMODWT",
-    "WaveletDenoiser", "ThresholdMethod", "ThresholdType",
+    "WaveletDenoiser", "ThresholdMethod", "ThresholdType", "BatchSIMDMODWT",
     "BatchStreamingMODWT", "Engine", "max_levels", "version",
 ]

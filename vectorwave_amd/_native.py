@@ -31,6 +31,7 @@ _fp = POINTER(c_float)
 SIGNATURES = {
     "vw_ctx_create": (c_int, [c_int, POINTER(c_void_p)]),
     "vw_ctx_destroy": (c_int, [c_void_p]),
+    "vw_ctx_use_null_stream": (c_int, [c_void_p]),
     "vw_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
     "vw_ctx_get_stream": (c_void_p, [c_void_p]),
     "vw_ctx_synchronize": (c_int, [c_void_p]),
@@ -56,6 +57,8 @@ SIGNATURES = {
                                    c_int, c_double, c_int, c_uint, c_void_p, c_void_p]),
     "vw_wavelet_denoise_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, _dp, _dp, c_int, c_int, c_int,
                                        c_int, c_int, c_double, c_int, c_uint, c_void_p, c_void_p]),
+    "vw_transpose_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_uint, c_void_p]),
+    "vw_transpose_f32": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_uint, c_void_p]),
     "vw_noise_sigma_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_uint, c_void_p]),
     "vw_threshold_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_int, c_uint]),
     "vw_stream_create": (c_int, [c_void_p, _dp, _dp, c_int, c_int, c_int, POINTER(c_void_p)]),

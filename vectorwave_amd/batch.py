@@ -108,6 +108,48 @@ class BatchMODWT:
                                         nat.FLAG_CORE_LEVELS | (nat.FLAG_FMA if fma else 0))
 
 
+class BatchSIMDMODWT:
+    """ext/extensions/modwt/BatchSIMDMODWT.java -- the facade's Structure-of-Arrays entry points.
+
+    SoA layout: one flat array, element t of signal b at index t*batchSize + b.  On the device the
+    layout change is a tiled transpose (vw_transpose_*, HBM-bound); the transforms run on the AoS
+    kernels, whose per-signal arithmetic is the reference's per-lane arithmetic (mul then add, taps
+    ascending).  Returns arrays instead of filling caller arrays.
+    """
+
+    @staticmethod
+    def convertToSoA(signals):
+        """convertToSoA :282-292: [B][N] -> flat [N*B]."""
+        x = _validate_aos(signals)
+        B, N = x.shape
+        return _engine_for(x).transpose(x, B, N)
+
+    @staticmethod
+    def convertFromSoA(soaData, batchSize: int, signalLength: int):
+        """convertFromSoA :299-308: flat [N*B] -> [B][N]."""
+        eng = _engine_for(soaData)
+        return eng.transpose(soaData, signalLength, batchSize).reshape(batchSize, signalLength)
+
+    @staticmethod
+    def batchMODWTSoA(soaSignals, wavelet: Wavelet, batchSize: int, signalLength: int, fma: bool = False):
+        """batchMODWTSoA :64-84 (Haar: 0.5/-0.5 taps :86-140).  Returns (soaApprox, soaDetail)."""
+        r = BatchMODWT.singleLevelAoS(wavelet, BatchSIMDMODWT.convertFromSoA(soaSignals, batchSize, signalLength),
+                                      fma=fma)
+        eng = _engine_for(r.approx)
+        return (eng.transpose(r.approx, batchSize, signalLength), eng.transpose(r.detail, batchSize, signalLength))
+
+    @staticmethod
+    def batchMultiLevelMODWTSoA(soaSignals, wavelet: Wavelet, batchSize: int, signalLength: int, levels: int,
+                                fma: bool = False):
+        """batchMultiLevelMODWTSoA :343-381.  Returns (soaDetailPerLevel [levels][N*B], soaApproxOut [N*B])."""
+        r = BatchMODWT.multiLevelAoS(wavelet, BatchSIMDMODWT.convertFromSoA(soaSignals, batchSize, signalLength),
+                                     levels, fma=fma)
+        eng = _engine_for(r.finalApprox)
+        det = [eng.transpose(r.detailPerLevel[j], batchSize, signalLength) for j in range(levels)]
+        stack = torch.stack if _is_device_tensor(r.finalApprox) else np.stack
+        return stack(det), eng.transpose(r.finalApprox, batchSize, signalLength)
+
+
 class BatchStreamingMODWT:
     """ext/extensions/modwt/BatchStreamingMODWT.java:19-400.
 

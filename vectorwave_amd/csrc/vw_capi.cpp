@@ -269,6 +269,21 @@ extern "C" vw_status vw_ctx_destroy(vw_ctx* c) {
   return ok();
 }
 
+// The device's null (legacy default) stream -- what torch uses when no stream is set: its handle is
+// 0, which vw_ctx_set_stream reads as "own stream".
+extern "C" vw_status vw_ctx_use_null_stream(vw_ctx* c) {
+  if (!c) return fail(VW_ERR_NULL, "ctx is null");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  if (c->own_stream) {
+    hipStreamSynchronize(c->stream);
+    hipStreamDestroy(c->stream);
+    c->own_stream = false;
+  }
+  c->stream = nullptr;
+  return ok();
+}
+
 extern "C" vw_status vw_ctx_set_stream(vw_ctx* c, void* s) {
   if (!c) return fail(VW_ERR_NULL, "ctx is null");
   std::lock_guard<std::recursive_mutex> g(c->mu);
@@ -934,6 +949,48 @@ extern "C" vw_status vw_threshold_f64(vw_ctx* c, double* coeffs, int64_t B, int6
   if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
   if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
   return ok();
+}
+
+// out[c][r] = in[r][c] (rows x cols).  AoS [B][N] -> SoA [N][B] is (rows=B, cols=N); back is
+// (rows=N, cols=B).  BatchSIMDMODWT.convertToSoA / convertFromSoA (BatchSIMDMODWT.java:282-308).
+template <typename T>
+static vw_status transpose_impl(vw_ctx* c, const T* in, int64_t rows, int64_t cols, unsigned flags, T* out) {
+  if (!c || !in || !out) return fail(VW_ERR_NULL, "null argument");
+  if (rows <= 0 || cols <= 0) return fail(VW_ERR_EMPTY, "empty input");
+  if (in == out) return fail(VW_ERR_ARG, "transpose is out of place");
+  if ((rows + 63) / 64 > 65535) return fail(VW_ERR_ARG, "rows %lld too large", (long long)rows);
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  const size_t n = (size_t)rows * (size_t)cols;
+  if (flags & VW_FLAG_HOST_MEMORY) {
+    Staging s(c);
+    T *di, *dout;
+    VW_TRY(s.in(in, n, &di));
+    VW_TRY(s.in<T>(nullptr, n, &dout));
+    hipError_t e = launch_transpose<T>(di, rows, cols, dout, c->stream);
+    if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+    VW_TRY(s.out(out, dout, n));
+    VW_HIP(hipStreamSynchronize(c->stream));
+    return ok();
+  }
+  hipError_t e;
+  {
+    LaunchTimer lt(c, "transpose");
+    e = launch_transpose<T>(in, rows, cols, out, c->stream);
+  }
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+  if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}
+
+extern "C" vw_status vw_transpose_f64(vw_ctx* c, const double* in, int64_t rows, int64_t cols, unsigned flags,
+                                      double* out) {
+  return transpose_impl<double>(c, in, rows, cols, flags, out);
+}
+
+extern "C" vw_status vw_transpose_f32(vw_ctx* c, const float* in, int64_t rows, int64_t cols, unsigned flags,
+                                      float* out) {
+  return transpose_impl<float>(c, in, rows, cols, flags, out);
 }
 
 static vw_status denoise_device(vw_ctx* c, const double* x, int64_t B, int64_t N, int64_t ldx, const double* lo,

@@ -155,6 +155,8 @@ hipError_t launch_level_threshold(const double* coeffs, long long level_stride, 
 hipError_t launch_noise_sigma(const double* coeffs, long long ld, long long B, int N, double scale_c,
                               double* sigma_out, double* thr_out, hipStream_t st);
 template <typename T>
+hipError_t launch_transpose(const T* in, long long rows, long long cols, T* out, hipStream_t st);
+template <typename T>
 hipError_t launch_threshold(T* c, long long B, long long N, const T* thr, int soft, hipStream_t st);
 template <typename T>
 hipError_t launch_fill_uniform(T* x, long long count, unsigned long long seed, long long offset, hipStream_t st);

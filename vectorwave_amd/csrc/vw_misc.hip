@@ -100,12 +100,45 @@ hipError_t launch_single_haar_batch(const T* x, long long ldx, long long B, int 
   return hipGetLastError();
 }
 
+// AoS <-> SoA layout change (BatchSIMDMODWT.convertToSoA / convertFromSoA, ext/extensions/modwt/
+// BatchSIMDMODWT.java:282-308): out[c][r] = in[r][c] for a rows x cols matrix, through 64 x 64 LDS
+// tiles (one padding column: conflict-free column reads), coalesced on both sides.  HBM-bound: 2 x
+// sizeof(T) bytes per element.
+constexpr int kTrTile = 64;
+template <typename T>
+__global__ void __launch_bounds__(256) k_transpose(const T* __restrict__ in, long long rows, long long cols,
+                                                   T* __restrict__ out) {
+  __shared__ T tile[kTrTile][kTrTile + 1];
+  const long long r0 = (long long)blockIdx.y * kTrTile, c0 = (long long)blockIdx.x * kTrTile;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;  // 64 x 4 threads
+#pragma unroll
+  for (int k = 0; k < kTrTile; k += 4) {
+    const long long r = r0 + ty + k, c = c0 + tx;
+    if (r < rows && c < cols) tile[ty + k][tx] = in[r * cols + c];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kTrTile; k += 4) {
+    const long long c = c0 + ty + k, r = r0 + tx;  // output row c, column r
+    if (r < rows && c < cols) out[c * rows + r] = tile[tx][ty + k];
+  }
+}
+
+template <typename T>
+hipError_t launch_transpose(const T* in, long long rows, long long cols, T* out, hipStream_t st) {
+  const dim3 grid((unsigned)((cols + kTrTile - 1) / kTrTile), (unsigned)((rows + kTrTile - 1) / kTrTile));
+  if (grid.y > 65535u) return hipErrorInvalidConfiguration;
+  hipLaunchKernelGGL(k_transpose<T>, grid, dim3(256), 0, st, in, rows, cols, out);
+  return hipGetLastError();
+}
+
 #define VW_INST(T)                                                                                              \
   template hipError_t launch_history_update<T>(const T*, long long, const T*, T*, long long, int, int,         \
                                                hipStream_t);                                                    \
   template hipError_t launch_threshold<T>(T*, long long, long long, const T*, int, hipStream_t);               \
   template hipError_t launch_fill_uniform<T>(T*, long long, unsigned long long, long long, hipStream_t);       \
-  template hipError_t launch_single_haar_batch<T>(const T*, long long, long long, int, T*, T*, hipStream_t);
+  template hipError_t launch_single_haar_batch<T>(const T*, long long, long long, int, T*, T*, hipStream_t); \
+  template hipError_t launch_transpose<T>(const T*, long long, long long, T*, hipStream_t);
 VW_INST(double)
 VW_INST(float)
 #undef VW_INST

@@ -63,7 +63,10 @@ class Engine:
         """Enqueue on torch's current stream of this device (orders engine work with torch ops)."""
         s = torch.cuda.current_stream(self.device).cuda_stream
         if s != self._ext_stream:
-            _check(self.lib.vw_ctx_set_stream(self.ctx, c_void_p(s)))
+            # torch's default stream has handle 0 (the null stream), which vw_ctx_set_stream would read
+            # as "use your own stream" -- unordered with torch's work
+            _check(self.lib.vw_ctx_use_null_stream(self.ctx) if s == 0 else
+                   self.lib.vw_ctx_set_stream(self.ctx, c_void_p(s)))
             self._ext_stream = s
 
     def synchronize(self) -> None:
@@ -195,6 +198,16 @@ class Engine:
                                                wavelet_id, boundary, levels, method, float(fixed), 1 if soft else 0,
                                                self._flags(flags, dev), self._ptr(y, dev), self._ptr(thr, dev)))
         return (y, thr) if want_thresholds else y
+
+    def transpose(self, a, rows: int, cols: int):
+        """out[c][r] = a[r][c] (a: rows*cols elements, any shape) -> flat [cols*rows] array."""
+        aa, dev, ap, f32 = self._prep(a)
+        if (aa.numel() if dev else aa.size) != rows * cols:
+            raise ValueError("transpose: size mismatch")
+        out = self._empty(aa, dev, (rows * cols,))
+        fn = self.lib.vw_transpose_f32 if f32 else self.lib.vw_transpose_f64
+        _check(fn(self.ctx, ap, rows, cols, self._flags(0, dev), self._ptr(out, dev)))
+        return out
 
     def noise_sigma(self, coeffs):
         ca, dev, cp, _ = self._prep(coeffs, np.float64)
