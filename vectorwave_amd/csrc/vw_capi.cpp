@@ -496,15 +496,28 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
   const int hlpad = (int)round_up(max_hl, V);
   int threads = 0, lds = 0, nv = 4;
   // Level buffers: two (one barrier per level) or one (two barriers per level, but half the LDS:
-  // twice the workgroups per CU).  Measured on MI355X (db4 J=6, 4096 x 4096 fp64): the exact kernel
-  // is faster with one buffer (more workgroups to overlap its longer arithmetic), the FMA kernel
-  // with two.  VW_FWD_BUF=1|2 overrides.
+  // twice the workgroups per CU).  Measured on MI355X (db4 J=6, 4096 x 4096 fp64): two buffers win
+  // whenever the persistent forward (which needs them) runs -- FMA and EXACT alike; without it the
+  // EXACT kernel is faster with one buffer (more workgroups to overlap its longer arithmetic).
+  // VW_FWD_BUF=1|2 overrides.
+  //
+  // Persistent variant (vw_device.h k_forward_persist): next row by LDS-DMA during the last level.
+  // Its contract: two buffers, full slabs of whole waves, rows in 64-vector chunks, no validation
+  // or streaming history.  VW_FWD_PERSIST=0 disables it.
+  const char* pe = getenv("VW_FWD_PERSIST");
+  const bool persist_on = !pe || atoi(pe) != 0;
+  const bool io_aligned = (ldx % V == 0) && (N % V == 0) && aligned16(x) && aligned16(details) && aligned16(approx);
+  auto persist_ok = [&](int th, int nvv, bool ft) {
+    return persist_on && io_aligned && ft && nvv == 4 && !validate && !hist && (int64_t)th * nvv == nvec &&
+           th % 64 == 0 && nvec % 64 == 0 && has_unrolled_taps(L) && J >= 1;
+  };
   const int64_t region = round_up(hlpad + nvec * V + V, V);
-  bool dbl = fma;
-  if (const char* e = getenv("VW_FWD_BUF")) dbl = atoi(e) == 2;
+  const char* fb = getenv("VW_FWD_BUF");
+  bool dbl = fb ? atoi(fb) == 2 : true;
   bool fused = false, fit = false;
   if (J <= kMaxLevels && !getenv("VW_FORCE_TILED")) {
     if (dbl) dbl = fused_plan(N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
+    if (dbl && !fb && !fma && !persist_ok(threads, nv, fit)) dbl = false;  // EXACT without persistence
     fused = dbl || fused_plan(N, V, sizeof(T), region, &threads, &nv, &lds, &fit);
   }
   if (fused) {
@@ -524,14 +537,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     copy_taps(a.hi, hi, L);
     for (int j = 0; j < J; ++j) a.lv[j] = lv[j];
     if (validate) VW_HIP(hipMemsetAsync(c->bad, 0xFF, sizeof(unsigned long long), c->stream));
-    // Persistent variant (vw_device.h k_forward_persist): next row by LDS-DMA during the last level.
-    // Its contract: two buffers, full slabs of whole waves, rows in 64-vector chunks, no validation
-    // or streaming history.  VW_FWD_PERSIST=0 disables it.
-    const char* pe = getenv("VW_FWD_PERSIST");
-    const bool persist_on = !pe || atoi(pe) != 0;
-    const bool persist = persist_on && dbl && a.unrolled && nv == 4 && !validate && !hist &&
-                         (int64_t)threads * nv == nvec && threads % 64 == 0 && nvec % 64 == 0 &&
-                         has_unrolled_taps(L) && J >= 1;
+    const bool persist = dbl && a.unrolled && persist_ok(threads, nv, fit);
     {
       LaunchTimer lt(c, "forward");
       hipError_t e = persist ? launch_forward_persist<T>(a, threads, lds, fma, c->stream)
