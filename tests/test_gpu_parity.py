@@ -444,3 +444,76 @@ def test_soa_single_and_multilevel_match_restatement(engine, w):
         d, a = O.decompose(x[b], *lohi(w), O.PERIODIC, J, core=False)
         exact(sdet.reshape(J, n, B)[:, :, b], d)
         exact(sapp.reshape(n, B)[:, b], a)
+
+
+# ---- core Flow-API streaming (MODWTStreamingTransform) --------------------------------------------------
+class _Collect:
+    def __init__(self):
+        self.items, self.done = [], False
+
+    def onNext(self, r):
+        self.items.append(r)
+
+    def onComplete(self):
+        self.done = True
+
+
+@pytest.mark.parametrize("w,buf", [(Daubechies.DB4, 64), (H, 16), (Symlet.SYM8, 100)], ids=["db4", "haar", "sym8"])
+@pytest.mark.parametrize("boundary", [O.PERIODIC, O.SYMMETRIC], ids=["P", "S"])
+def test_streaming_transform_windows(engine, w, buf, boundary):
+    """MODWTStreamingTransformImpl: windows of bufferSize overlapping by L-1 (:188-218), flush zero-pads the
+    rest (:228-252); chunks of any size (one batched device call per process())."""
+    rng = np.random.default_rng(buf)
+    x = rng.standard_normal(1000)
+    st = vw.MODWTStreamingTransform.create(w, vw.BoundaryMode(boundary), buf)
+    sub = _Collect()
+    st.subscribe(sub)
+    pos = 0
+    for n in (1, 7, buf - 1, 3 * buf + 5, 250, 1):
+        st.process(x[pos:pos + n])
+        pos += n
+    st.process(x[pos:])
+    st.close()
+    L = len(w.lowPassDecomposition())
+    hop = buf - (L - 1)
+    starts = list(range(0, len(x) - buf + 1, hop))
+    rem = len(x) - (starts[-1] + hop)
+    assert sub.done and len(sub.items) == len(starts) + (1 if rem > 0 else 0)
+    for r, s0 in zip(sub.items, starts):
+        a, d = O.modwt_forward(x[s0:s0 + buf], *lohi(w), boundary)
+        exact(r.approximationCoeffs(), a)
+        exact(r.detailCoeffs(), d)
+    if rem > 0:
+        tail = np.zeros(buf)
+        tail[:rem] = x[len(x) - rem:]
+        a, d = O.modwt_forward(tail, *lohi(w), boundary)
+        exact(sub.items[-1].approximationCoeffs(), a)
+    assert st.getStatistics().getSamplesProcessed() == len(x)
+    with pytest.raises(vw.InvalidStateException):
+        st.process(x[:4])
+
+
+def test_streaming_multilevel_blocks(engine):
+    """MultiLevelMODWTStreamingTransform: non-overlapping blocks, one result per level, approximation
+    only at the last level (:133-166, :238-240)."""
+    w, buf, J = Daubechies.DB4, 128, 3
+    x = np.random.default_rng(5).standard_normal(3 * buf + 40)
+    st = vw.MODWTStreamingTransform.createMultiLevel(w, vw.BoundaryMode.PERIODIC, buf, J)
+    got = []
+    st.subscribe(got.append)
+    st.process(x[:100])
+    st.process(x[100:])
+    st.flush()
+    blocks = [x[k * buf:(k + 1) * buf] for k in range(3)] + [np.concatenate([x[3 * buf:], np.zeros(buf - 40)])]
+    assert len(got) == 4 * J
+    for k, blk in enumerate(blocks):
+        d, a = O.decompose(blk, *lohi(w), O.PERIODIC, J)
+        for j in range(J):
+            r = got[k * J + j]
+            exact(r.detailCoeffs(), d[j])
+            assert r.approximationCoeffs().size == (buf if j == J - 1 else 0)
+        exact(got[k * J + J - 1].approximationCoeffs(), a)
+    with pytest.raises(vw.InvalidArgumentException):
+        vw.MODWTStreamingTransform.createMultiLevel(w, vw.BoundaryMode.PERIODIC, buf, 0)
+    with pytest.raises(vw.InvalidArgumentException):
+        vw.MODWTStreamingTransform.create(w, vw.BoundaryMode.PERIODIC, 4)  # bufferSize < filter length

@@ -7,6 +7,7 @@ include/vectorwave_amd.h).  This package is the host-side mirror of the referenc
   MutableMultiLevelMODWTResult, BoundaryMode                  (core/modwt, core/api)
   VectorWaveSwtAdapter                                        (core/swt)
   WaveletDenoiser                                             (core/denoising)
+  MODWTStreamingTransform, MultiLevelMODWTStreamingTransform  (core/modwt/streaming)
   BatchMODWT, BatchStreamingMODWT                             (ext/extensions/modwt)
   Haar, Daubechies, Symlet, Coiflet                           (core/api wavelets)
 """
@@ -17,6 +18,7 @@ from .modwt import (BoundaryMode, MODWTResult, MODWTTransform, MultiLevelMODWTRe
                     MutableMultiLevelMODWTResult)
 from .swt import VectorWaveSwtAdapter
 from .denoise import ThresholdMethod, ThresholdType, WaveletDenoiser
+from .streaming import MODWTStreamingTransform, MODWTStreamingTransformImpl, MultiLevelMODWTStreamingTransform
 from .batch import BatchMODWT, BatchSIMDMODWT, BatchStreamingMODWT
 from .engine import Engine, max_levels, version
 
@@ -25,6 +27,7 @@ __all__ = [
     "ErrorCode", "InvalidArgumentException", "InvalidSignalException", "InvalidStateException",
     "WaveletTransformException", "BoundaryMode", "MODWTResult", "MODWTTransform", "MultiLevelMODWTResult",
     "MultiLevelMODWTTransform", "MutableMultiLevelMODWTResult", "VectorWaveSwtAdapter", "BatchMODWT",
-    "WaveletDenoiser", "ThresholdMethod", "ThresholdType", "BatchSIMDMODWT",
+    "WaveletDenoiser", "ThresholdMethod", "ThresholdType", "BatchSIMDMODWT", "MODWTStreamingTransform",
+    "MODWTStreamingTransformImpl", "MultiLevelMODWTStreamingTransform",
     "BatchStreamingMODWT", "Engine", "max_levels", "version",
 ]
