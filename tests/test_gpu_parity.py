@@ -517,3 +517,28 @@ def test_streaming_multilevel_blocks(engine):
         vw.MODWTStreamingTransform.createMultiLevel(w, vw.BoundaryMode.PERIODIC, buf, 0)
     with pytest.raises(vw.InvalidArgumentException):
         vw.MODWTStreamingTransform.create(w, vw.BoundaryMode.PERIODIC, 4)  # bufferSize < filter length
+
+
+def test_forward_strided_rows_ldx(engine):
+    """vw_modwt_forward_f64 with ldx > N (rows of a wider buffer, e.g. a strided JNI view): the
+    persistent forward's row DMA and the per-signal kernels address row b at x + b*ldx."""
+    import ctypes
+    import torch
+    w = Daubechies.DB4
+    B, N, J, pad = 600, 4096, 6, 64
+    big = torch.empty((B, N + pad), dtype=torch.float64, device="cuda")
+    engine.fill_uniform(big, 9)
+    x = big[:, :N].contiguous()
+    lib = nat.load()
+    for flags in (nat.FLAG_FMA, 0):
+        det = torch.empty((J, B, N), dtype=torch.float64, device="cuda")
+        app = torch.empty((B, N), dtype=torch.float64, device="cuda")
+        st = lib.vw_modwt_forward_f64(engine.ctx, ctypes.c_void_p(big.data_ptr()), B, N, N + pad,
+                                      nat.taps_array(w.lowPassDecomposition()), nat.taps_array(w.highPassDecomposition()),
+                                      8, w.wavelet_id, O.PERIODIC, J, flags, ctypes.c_void_p(det.data_ptr()),
+                                      ctypes.c_void_p(app.data_ptr()))
+        assert st == 0
+        d2, a2 = engine.forward(x, w.lowPassDecomposition(), w.highPassDecomposition(), w.wavelet_id, O.PERIODIC, J,
+                                flags)
+        torch.cuda.synchronize()
+        assert torch.equal(det, d2) and torch.equal(app, a2)
