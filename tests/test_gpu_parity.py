@@ -373,6 +373,33 @@ def test_tiled_path_bit_exact(engine, monkeypatch):
                                       w.wavelet_id))
 
 
+@pytest.mark.parametrize("tile", ["128", "2048"])
+def test_multilevel_tiles_bit_exact(engine, monkeypatch, tile):
+    # long PERIODIC signals run groups of levels per tile (vw_capi.cpp level_groups): odd N (scalar
+    # I/O), N not a multiple of the tile, tiles shorter than the reach (wraps through the halo), and
+    # the SWT denoise thresholds applied on the detail loads; EXACT mode is bit-exact
+    monkeypatch.setenv("VW_FORCE_TILED", "1")
+    monkeypatch.setenv("VW_MULTI_TILE", tile)
+    for w, n, J in [(Daubechies.DB4, 10000, 6), (Daubechies.DB8, 30001, 8), (H, 5000, 9),
+                    (Coiflet.COIF5, 20000, 5), (Symlet.SYM8, 4097, 6)]:   # J=7 would enter the FFT region
+        x = signals(2, n, 23)
+        tx = vw.MultiLevelMODWTTransform(w, vw.BoundaryMode.PERIODIC)
+        res = tx.decompose(x, J)
+        y = tx.reconstruct(res)
+        for b in range(2):
+            d, a = O.decompose(x[b], *lohi(w), O.PERIODIC, J)
+            exact(res.details_array[:, b, :], d)
+            exact(res.approximation_array[b], a)
+            exact(y[b], O.reconstruct(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC))
+    w, n, J = Symlet.SYM8, 12000, 5
+    x = signals(2, n, 29)
+    y, thr = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC).denoise(x, J, return_thresholds=True)
+    for b in range(2):
+        y_ref, t_ref = O.swt_denoise(x[b], *lohi(w), O.PERIODIC, J, wavelet_id=w.wavelet_id)
+        assert thr[b] == t_ref
+        exact(y[b], y_ref)
+
+
 def test_long_block_db8_j10(engine):
     # config 4 shape on a short batch: 2^17-sample PERIODIC block, db8, J=10 (BatchMODWT semantics)
     w = Daubechies.DB8

@@ -456,6 +456,45 @@ static void set_halo_images(LevelDesc& d, int64_t N, int64_t npow2, int V, int t
   d.own = (d.hl <= N && d.hr <= N && d.vs <= threads && (int64_t)d.ve >= (int64_t)(nv - 1) * threads) ? 1 : 0;
 }
 
+// Level groups of the per-level path (vw_device.h k_forward_multi / k_inverse_multi): from level 1
+// up, consecutive PERIODIC levels run as one multi-level tile launch while their combined reach
+// sum((L-1)*s_j) stays within a quarter of the tile (the redundant arithmetic).  groups[j-1] = size
+// of the group starting at level j (0 inside a group, 1 = the per-level kernels).  VW_MULTI=0
+// disables; VW_MULTI_TILE / VW_MULTI_DIV tune tile and reach bound.
+template <typename T>
+static int multi_tile() {
+  constexpr int V = vec_width<T>();
+  const char* e = getenv("VW_MULTI_TILE");
+  const int v = e ? atoi(e) : (int)(16384 / sizeof(T));
+  return v >= 64 * V ? v / V * V : 64 * V;
+}
+
+static std::vector<int> level_groups(const std::vector<LevelDesc>& lv, int J, int L, int V, int tile, bool ok) {
+  std::vector<int> g(J, 1);
+  const char* en = getenv("VW_MULTI");
+  if (!ok || (en && atoi(en) == 0)) return g;
+  const char* dv = getenv("VW_MULTI_DIV");
+  const int64_t cap = tile / std::max(1, dv ? atoi(dv) : 4);
+  for (int j = 1; j <= J;) {
+    int n = 0;
+    int64_t ext = 0;
+    while (j + n <= J && n < kMaxGroup && lv[j + n - 1].mode == kHaloPeriodic) {
+      const int64_t e2 = ext + round_up((int64_t)(L - 1) * lv[j + n - 1].s, V);
+      if (e2 > cap) break;
+      ext = e2;
+      ++n;
+    }
+    if (n >= 2) {
+      g[j - 1] = n;
+      for (int k = 1; k < n; ++k) g[j - 1 + k] = 0;
+      j += n;
+    } else {
+      ++j;
+    }
+  }
+  return g;
+}
+
 // ------------------------------------------------------------------------------------------------
 // Forward (multi-level and single-level share this path).
 template <typename T>
@@ -557,7 +596,40 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     if (validate) VW_HIP(hipMemsetAsync(c->bad, 0xFF, sizeof(unsigned long long), c->stream));
     const T* src = x;
     int64_t lda = ldx;
+    const int mtile = multi_tile<T>();
+    const std::vector<int> groups = level_groups(lv, J, L, V, mtile, !validate && !hist);
     for (int j = 1; j <= J; ++j) {
+      T* const nxt = (src == tmp[0]) ? tmp[1] : tmp[0];  // never the level's own input
+      if (groups[j - 1] >= 2) {
+        const int g = groups[j - 1], je = j + g - 1;
+        MultiArgs<T> m;
+        memset(&m, 0, sizeof(m));
+        m.src_a = src; m.lda = lda;
+        m.out_a = (je == J) ? approx : nxt;
+        bool al = aligned16(src) && aligned16(m.out_a);
+        for (int k = 0; k < g; ++k) {
+          m.out_d[k] = details + (size_t)(j - 1 + k) * plane;
+          al = al && aligned16(m.out_d[k]);
+        }
+        m.ext[g] = 0;
+        for (int k = g - 1; k >= 0; --k)
+          m.ext[k] = m.ext[k + 1] + (int)round_up((int64_t)(L - 1) * lv[j - 1 + k].s, V);
+        m.B = B; m.N = (int)N; m.tile = mtile; m.nlev = g; m.s0 = lv[j - 1].s;
+        m.region = (int)round_up(m.ext[0] + mtile + V, V);
+        m.vec_io = (N % V == 0) && (lda % V == 0) && al;
+        m.taps = L;
+        copy_taps(m.lo, lo, L);
+        copy_taps(m.hi, hi, L);
+        {
+          LaunchTimer lt(c, "forward_level");
+          hipError_t e = launch_forward_multi<T>(m, (int)(2 * m.region * sizeof(T)), fma, c->stream);
+          if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward multi-level launch failed: %s", hipGetErrorString(e));
+        }
+        src = m.out_a;
+        lda = N;
+        j = je;
+        continue;
+      }
       LevelArgs<T> a;
       memset(&a, 0, sizeof(a));
       a.lv = lv[j - 1];
@@ -568,7 +640,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
       if (tile < 64 * V) return fail(VW_ERR_UNSUPPORTED, "level %d halo (%d samples) exceeds LDS", j, a.lv.hl);
       const int64_t elems = hp + tile + V;
       a.src_a = src; a.lda = lda;
-      a.out_a = (j == J) ? approx : tmp[j & 1];
+      a.out_a = (j == J) ? approx : nxt;
       a.out_d = details + (size_t)(j - 1) * plane;
       a.hist = hist ? hist[j - 1] : nullptr;
       a.B = B; a.N = (int)N; a.tile = tile; a.hlpad = hp;
@@ -697,7 +769,45 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     if (st != VW_OK) return st;
     T* tmp[2] = {reinterpret_cast<T*>(c->ws), reinterpret_cast<T*>(c->ws) + plane};
     const T* cur = approx_zero ? nullptr : approx;
+    // multi-level groups (PERIODIC sequential sums): start level of the group whose top is j
+    const int mtile = multi_tile<T>();
+    const std::vector<int> groups = level_groups(lv, J, L, V, mtile, !pair && boundary == VW_PERIODIC);
+    std::vector<int> start_of(J + 1, 0);
+    for (int j = 1; j <= J; ++j) {
+      if (groups[j - 1] < 2) continue;
+      int64_t ext = 0;  // k_inverse_multi holds (tile + reach) / V vectors in kMultiInvNI per thread
+      for (int k = 0; k < groups[j - 1]; ++k) ext += round_up((int64_t)(L - 1) * lv[j - 1 + k].s, V);
+      if ((mtile + ext) / V <= (int64_t)kMultiInvNI * 256) start_of[j + groups[j - 1] - 1] = j;
+    }
     for (int j = J; j >= 1; --j) {
+      T* const nxt = (cur == tmp[0]) ? tmp[1] : tmp[0];  // never the level's own input
+      if (start_of[j] > 0) {
+        const int j0 = start_of[j], g = j - j0 + 1;
+        MultiArgs<T> m;
+        memset(&m, 0, sizeof(m));
+        m.src_a = cur;
+        m.out_a = (j0 == 1) ? y : nxt;
+        bool al = aligned16(cur) && aligned16(m.out_a);
+        for (int k = 0; k < g; ++k) {
+          const LevelDesc& d = lv[j0 - 1 + k];
+          m.src_d[k] = d.use_d ? details + (size_t)(j0 - 1 + k) * plane : nullptr;
+          m.thr[k] = thr ? thr + (size_t)(j0 - 1 + k) * (size_t)thr_ld : nullptr;
+          al = al && aligned16(m.src_d[k]);
+          m.ext[k] = (k > 0 ? m.ext[k - 1] : 0) + (int)round_up((int64_t)(L - 1) * d.s, V);
+        }
+        m.B = B; m.N = (int)N; m.tile = mtile; m.nlev = g; m.s0 = lv[j0 - 1].s;
+        m.region = (int)round_up(mtile + m.ext[g - 1] + V, V);
+        m.vec_io = (N % V == 0) && al;
+        m.soft = soft; m.taps = L;
+        copy_taps(m.lo, lo, L);
+        copy_taps(m.hi, hi, L);
+        LaunchTimer lt(c, "inverse_level");
+        hipError_t e = launch_inverse_multi<T>(m, (int)(2 * m.region * sizeof(T)), fma, c->stream);
+        if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse multi-level launch failed: %s", hipGetErrorString(e));
+        cur = m.out_a;
+        j = j0;
+        continue;
+      }
       LevelArgs<T> a;
       memset(&a, 0, sizeof(a));
       a.lv = lv[j - 1];
@@ -709,7 +819,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       a.src_a = cur;
       a.src_d = a.lv.use_d ? details + (size_t)(j - 1) * plane : nullptr;
       a.use_d = a.lv.use_d;
-      a.out_a = (j == 1) ? y : tmp[j & 1];
+      a.out_a = (j == 1) ? y : nxt;
       a.B = B; a.N = (int)N; a.tile = tile; a.hlpad = hp; a.hlpad_d = hp; a.region_d = (int)reg;
       a.pair = pair; a.thr = thr ? thr + (size_t)(j - 1) * (size_t)thr_ld : nullptr; a.soft = soft; a.taps = L;
       a.vec_io = (N % V == 0) && aligned16(a.out_a) && aligned16(a.src_a) && aligned16(a.src_d);

@@ -1236,6 +1236,117 @@ __global__ void __launch_bounds__(256) k_inverse_sweep(const LevelArgs<T> p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Multi-level tiles for long PERIODIC signals (host: vw_capi.cpp level_groups).  One workgroup runs
+// a group of consecutive levels over one tile of one signal; the intermediate approximations stay
+// in LDS.  Periodic convolution commutes with shifts, so a level evaluated at a position v outside
+// [0, N) (the tile's halo) equals the reference's value at v mod N bit for bit -- the same products
+// summed in the same order -- and only the group's inputs go through the index map.  Each level is
+// evaluated over the tile plus the reach of the levels after it: to the left in the forward
+// (ScalarOps.java:700-723 reads t - l*s), to the right in the inverse (MultiLevelMODWTTransform
+// .java:576-589 reads t + l*s).  The redundant ext/tile of the arithmetic buys one HBM round trip
+// per group instead of one per level.
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(256) k_forward_multi(const MultiArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* X = reinterpret_cast<T*>(smem) + p.ext[0];  // level input, positions [-ext[k], span)
+  T* Y = X + p.region;
+  const long long b = blockIdx.y;
+  const int N = p.N;
+  const int ts = blockIdx.x * p.tile;
+  const int cnt = min(p.tile, N - ts);
+  const int span = (cnt + V - 1) / V * V;
+  const bool vec_ok = p.vec_io != 0;
+  tile_to_lds(X, p.src_a + b * p.lda, N, ts, -p.ext[0], span, kHaloPeriodic, 0, (const T*)nullptr, 0,
+              (const T*)nullptr, T(0), 0, false, vec_ok);
+  for (int k = 0; k < p.nlev; ++k) {
+    lds_barrier();  // X complete; every read of Y (the previous level's input) done
+    const int s = p.s0 << k;
+    const int q_lo = -p.ext[k + 1];  // outputs [q_lo, span): the tile + what the next levels read
+    const int nv = (span - q_lo) / V;
+    const bool last = k == p.nlev - 1;
+    T* od = p.out_d[k] + b * (size_t)N + ts;
+    T* oa = p.out_a + b * (size_t)N + ts;
+    for (int w = threadIdx.x; w < nv; w += blockDim.x) {
+      const int q0 = q_lo + w * V;
+      T al[V], ah[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) { al[e] = T(0); ah[e] = T(0); }
+      fwd_vec<T, L, FMA>(X, q0, s, p.lo, p.hi, p.taps, al, ah);
+      if (q0 >= 0) {  // the tile's own outputs (vectors never straddle 0: q_lo is a multiple of V)
+        store_vec(od, q0, cnt, vec_ok, ah);
+        if (last) store_vec(oa, q0, cnt, vec_ok, al);
+      }
+      if (!last) {
+        vec o;
+#pragma unroll
+        for (int e = 0; e < V; ++e) o[e] = al[e];
+        *reinterpret_cast<vec*>(Y + q0) = o;
+      }
+    }
+    T* t = X; X = Y; Y = t;
+  }
+}
+
+// Inverse: A = a_j, D = d_j (thresholded on load for denoise); a_{j-1} is computed into registers
+// (kMultiInvNI vectors per thread) and written over A after a barrier -- two LDS regions, so four
+// 256-thread workgroups fit a CU (a third region for a_{j-1} measured 1.2x slower: two per CU).
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  constexpr int NI = kMultiInvNI;  // host contract: (tile + ext[top]) / V <= NI * 256
+  using vec = typename VT<T>::v;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* const A = reinterpret_cast<T*>(smem);  // positions [0, span + ext[k])
+  T* const D = A + p.region;
+  const long long b = blockIdx.y;
+  const int N = p.N;
+  const int ts = blockIdx.x * p.tile;
+  const int cnt = min(p.tile, N - ts);
+  const int span = (cnt + V - 1) / V * V;
+  const bool vec_ok = p.vec_io != 0;
+  const int top = p.nlev - 1;
+  tile_to_lds(A, p.src_a ? p.src_a + b * (size_t)N : p.src_a, N, ts, 0, span + p.ext[top], kHaloPeriodic, 0,
+              (const T*)nullptr, 0, (const T*)nullptr, T(0), 0, p.src_a == nullptr, vec_ok);
+  for (int k = top; k >= 0; --k) {
+    const T* sd = p.src_d[k];
+    const T* th = p.thr[k];
+    tile_to_lds(D, sd ? sd + b * (size_t)N : sd, N, ts, 0, span + p.ext[k], kHaloPeriodic, 0, (const T*)nullptr, 0,
+                th, th ? th[b] : T(0), p.soft, sd == nullptr, vec_ok);
+    lds_barrier();  // A and D complete
+    const int s = p.s0 << k;
+    const int nv = (span + (k > 0 ? p.ext[k - 1] : 0)) / V;  // the tile + what the next levels read
+    T acc[NI][V];
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int w = threadIdx.x + i * 256;
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[i][e] = T(0);
+      if (w < nv) {
+        // K4: all approximation taps, then all detail taps, into one accumulator
+        inv_branch<T, L, FMA>(A, w * V, s, 1, 0, p.lo, p.taps, acc[i]);
+        inv_branch<T, L, FMA>(D, w * V, s, 1, 0, p.hi, p.taps, acc[i]);
+        if (k == 0) store_vec(p.out_a + b * (size_t)N + ts, w * V, cnt, vec_ok, acc[i]);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // one vector's LDS reads in flight at a time (VGPR budget)
+    }
+    if (k == 0) break;
+    lds_barrier();  // every read of A and D done
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int w = threadIdx.x + i * 256;
+      if (w < nv) {
+        vec o;
+#pragma unroll
+        for (int e = 0; e < V; ++e) o[e] = acc[i][e];
+        *reinterpret_cast<vec*>(A + w * V) = o;
+      }
+    }
+  }
+}
+
 template <typename T>
 __global__ void k_history_update(const T* __restrict__ in, long long ld_in, const T* __restrict__ old_hist,
                                  T* __restrict__ new_hist, int n, int hist_len) {

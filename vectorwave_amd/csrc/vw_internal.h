@@ -119,6 +119,34 @@ struct LevelArgs {
   LevelDesc lv;
 };
 
+// Multi-level tiles (PERIODIC, long signals): a group of consecutive levels of one tile in one
+// launch, the intermediate approximations kept in LDS (vw_device.h k_forward_multi / k_inverse_multi).
+constexpr int kMaxGroup = 8;
+constexpr int kMultiInvNI = 8;  // k_inverse_multi: output vectors per thread (256 threads)
+template <typename T>
+struct MultiArgs {
+  const T* src_a;            // forward: input of the group's first level [B][lda]; inverse: a_{j1} [B][N] (nullptr = 0)
+  long long lda;
+  const T* src_d[kMaxGroup]; // inverse: d_j of group level k (k = 0 is the finest), nullptr = zero
+  T* out_d[kMaxGroup];       // forward: d_j of group level k
+  T* out_a;                  // forward: approximation of the coarsest level; inverse: a_{j0-1}
+  const T* thr[kMaxGroup];   // inverse denoise: thresholds [B] of group level k (nullptr = none)
+  long long B;
+  int N;
+  int tile;                  // stored outputs per workgroup (multiple of V)
+  int nlev;                  // levels in the group
+  int s0;                    // spacing of the group's finest level
+  int ext[kMaxGroup + 1];    // forward: left extent of level k's input (ext[nlev] = 0);
+                             // inverse: right extent of level k's input;
+                             // multiples of V, each covering the reach of the levels after it
+  int region;                // element stride between LDS buffers
+  int vec_io;
+  int soft;
+  int taps;
+  T lo[kMaxTaps];
+  T hi[kMaxTaps];
+};
+
 // WaveletDenoiser threshold methods (core/denoising/WaveletDenoiser.java:588-622) and the per-launch
 // constants of the threshold kernels (vw_sigma.h).
 enum ThrMethod { kThrUniversal = 0, kThrSure = 1, kThrMinimax = 2, kThrBayes = 3, kThrFixed = 4 };
@@ -146,6 +174,10 @@ template <typename T>
 hipError_t launch_forward_sweep(const LevelArgs<T>& a, bool fma, hipStream_t st);
 template <typename T>
 hipError_t launch_inverse_sweep(const LevelArgs<T>& a, bool fma, hipStream_t st);
+template <typename T>
+hipError_t launch_forward_multi(const MultiArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
+template <typename T>
+hipError_t launch_inverse_multi(const MultiArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
 template <typename T>
 hipError_t launch_history_update(const T* level_in, long long ld_in, const T* old_hist, T* new_hist,
                                  long long B, int n, int hist_len, hipStream_t st);

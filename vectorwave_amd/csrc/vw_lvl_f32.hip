@@ -114,3 +114,5 @@ hipError_t launch_inverse_level(const LevelArgs<T>& a, int lds, bool fma, hipStr
 template hipError_t launch_forward_level<VW_T>(const LevelArgs<VW_T>&, int, bool, hipStream_t);
 template hipError_t launch_inverse_level<VW_T>(const LevelArgs<VW_T>&, int, bool, hipStream_t);
 }  // namespace vw
+
+#include "vw_multi.inc"
