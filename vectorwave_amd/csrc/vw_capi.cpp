@@ -799,6 +799,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         m.region = (int)round_up(mtile + m.ext[g - 1] + V, V);
         m.vec_io = (N % V == 0) && al;
         m.soft = soft; m.taps = L;
+        { const char* rb = getenv("VW_MULTI_RBLK"); m.rblk = rb ? atoi(rb) : 1; }
         copy_taps(m.lo, lo, L);
         copy_taps(m.hi, hi, L);
         LaunchTimer lt(c, "inverse_level");

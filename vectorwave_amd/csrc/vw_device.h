@@ -1319,6 +1319,59 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
     const int s = p.s0 << k;
     const int nv = (span + (k > 0 ? p.ext[k - 1] : 0)) / V;  // the tile + what the next levels read
     T acc[NI][V];
+    if constexpr (L > 0) {
+      // Register-blocked taps (S a multiple of V): one thread owns the NI outputs v, v+m, .., v+(NI-1)m
+      // (m = S/V vectors), which read the same LDS vectors shifted by one tap: NI+L-1 reads per branch
+      // instead of NI*L.  Per output the taps still run i ascending, A then D: bit-identical sums.
+      const int m = s / V;
+      const int pairs = (nv + m * NI - 1) / (m * NI) * m;  // (block, column) pairs, uniform
+      if (p.rblk && s >= V && s % V == 0 && pairs <= 256) {
+        const int pr = threadIdx.x;
+        const int vb = (pr / m) * m * NI + pr % m;
+        const int lim = (span + p.ext[k]) / V - 1;  // last vector of the A/D regions
+#pragma unroll
+        for (int r = 0; r < NI; ++r)
+#pragma unroll
+          for (int e = 0; e < V; ++e) acc[r][e] = T(0);
+        if (pr < pairs) {
+#pragma unroll
+          for (int br = 0; br < 2; ++br) {
+            const T* buf = br == 0 ? A : D;
+            const T* f = br == 0 ? p.lo : p.hi;
+#pragma unroll
+            for (int j = 0; j < NI + L - 1; ++j) {
+              const vec x = *reinterpret_cast<const vec*>(buf + min(vb + m * j, lim) * V);
+#pragma unroll
+              for (int r = 0; r < NI; ++r) {
+                const int i = j - r;
+                if (i >= 0 && i < L)
+#pragma unroll
+                  for (int e = 0; e < V; ++e) acc[r][e] = madd<FMA>(acc[r][e], x[e], f[i]);
+              }
+            }
+          }
+          if (k == 0) {
+#pragma unroll
+            for (int r = 0; r < NI; ++r)
+              if (vb + m * r < nv) store_vec(p.out_a + b * (size_t)N + ts, (vb + m * r) * V, cnt, vec_ok, acc[r]);
+          }
+        }
+        if (k == 0) break;
+        lds_barrier();  // every read of A and D done
+        if (pr < pairs) {
+#pragma unroll
+          for (int r = 0; r < NI; ++r) {
+            if (vb + m * r < nv) {
+              vec o;
+#pragma unroll
+              for (int e = 0; e < V; ++e) o[e] = acc[r][e];
+              *reinterpret_cast<vec*>(A + (vb + m * r) * V) = o;
+            }
+          }
+        }
+        continue;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int w = threadIdx.x + i * 256;

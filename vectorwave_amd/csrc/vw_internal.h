@@ -143,6 +143,7 @@ struct MultiArgs {
   int vec_io;
   int soft;
   int taps;
+  int rblk;                  // inverse: register-blocked taps where S is a multiple of V
   T lo[kMaxTaps];
   T hi[kMaxTaps];
 };
