@@ -233,6 +233,22 @@ VW_API vw_status vw_stream_flush_f64(vw_stream *s, int64_t tail_len, unsigned fl
                                      double *details, double *approx);
 VW_API int64_t vw_stream_history_length(vw_stream *s, int level);
 
+/* ---- captured steps ------------------------------------------------------- */
+/* A caller that repeats the same calls on the same buffers (a JNI server's per-batch loop, a
+ * benchmark) records them once and replays them with one host call: host planning, argument
+ * packing and the per-kernel launch cost are paid at capture.  Between vw_capture_begin and
+ * vw_capture_end the context's calls are recorded (HIP stream capture of the context stream),
+ * not run; calls that must synchronize (VW_FLAG_VALIDATE, VW_FLAG_HOST_MEMORY, VW_FLAG_SYNC, a
+ * fixed denoise threshold, stream flush, workspace growth) fail with VW_ERR_STATE.  The context
+ * must be bound to a stream other than the null stream.  No reference counterpart: the Java
+ * callers re-enter per call; this is the device-side amortisation of that loop. */
+typedef struct vw_graph vw_graph;
+VW_API vw_status vw_capture_begin(vw_ctx *ctx);
+VW_API vw_status vw_capture_end(vw_ctx *ctx, vw_graph **out);
+/* Replays the recorded calls `count` times, in order, on the context's stream (asynchronous). */
+VW_API vw_status vw_graph_launch(vw_graph *graph, int64_t count);
+VW_API vw_status vw_graph_destroy(vw_graph *graph);
+
 /* ---- device utilities ---------------------------------------------------- */
 /* x[i] = 2*u - 1 with u = (splitmix64(seed ^ (offset + i)) >> 11) * 2^-53. */
 VW_API vw_status vw_fill_uniform_f64(vw_ctx *ctx, double *x, int64_t count, uint64_t seed, int64_t offset);

@@ -107,10 +107,15 @@ int vwo_symmetric_index(int idx, int n)
     return idx;
 }
 
+/* Long rows: the per-output loops below run OpenMP-parallel over t (n >= 32768).  Each output is
+ * still one sequential sum in the reference's order, so results are bit-identical to the serial
+ * loops; inside an outer parallel region (batch over rows) they stay serial (no nesting). */
+
 /* ---------------------------------------------------------------- A6 ---- */
 /* ScalarOps.circularConvolveMODWTScalar  core/internal/ScalarOps.java:700-723 */
 void vwo_circular_conv(const double *signal, int n, const double *filter, int fl, double *out)
 {
+    #pragma omp parallel for schedule(static) if (n >= 32768)
     for (int t = 0; t < n; t++) {
         double sum = 0.0;
         for (int l = 0; l < fl; l++) {
@@ -129,6 +134,7 @@ void vwo_circular_conv(const double *signal, int n, const double *filter, int fl
 void vwo_circular_conv_direct(const double *signal, int n, const double *filter, int fl, double *out)
 {
     int eff = fl < n ? fl : n;
+    #pragma omp parallel for schedule(static) if (n >= 32768)
     for (int t = 0; t < n; t++) {
         double sum = 0.0;
         int maxk = eff < t + 1 ? eff : t + 1;
@@ -141,6 +147,7 @@ void vwo_circular_conv_direct(const double *signal, int n, const double *filter,
 /* ScalarOps.zeroPaddingConvolveMODWT  core/internal/ScalarOps.java:790-808 */
 void vwo_zero_conv(const double *signal, int n, const double *filter, int fl, double *out)
 {
+    #pragma omp parallel for schedule(static) if (n >= 32768)
     for (int t = 0; t < n; t++) {
         double sum = 0.0;
         for (int l = 0; l < fl; l++) {
@@ -154,6 +161,7 @@ void vwo_zero_conv(const double *signal, int n, const double *filter, int fl, do
 /* ScalarOps.symmetricConvolveMODWT  core/internal/ScalarOps.java:818-835 */
 void vwo_symmetric_conv(const double *signal, int n, const double *filter, int fl, double *out)
 {
+    #pragma omp parallel for schedule(static) if (n >= 32768)
     for (int t = 0; t < n; t++) {
         double sum = 0.0;
         for (int l = 0; l < fl; l++) {
@@ -336,6 +344,7 @@ int vwo_ml_decompose(const double *x, int n, const double *lo, const double *hi,
             /* BatchSIMDMODWT.generalBatchMODWTSoAWithScaledFilters :384-424 -- srcT = (t - l + N) % N */
             if (fl > n + 1) { st = VWO_ERR_TOO_LARGE; break; } /* Java would index out of bounds */
             double *d = details + (size_t)(level - 1) * n;
+            #pragma omp parallel for schedule(static) if (n >= 32768)
             for (int t = 0; t < n; t++) {
                 double as = 0.0, ds = 0.0;
                 for (int l = 0; l < fl; l++) {
@@ -416,6 +425,7 @@ static int apply_scaled_inverse(const double *a, const double *d, int n, const d
 {
     if (fl > n) return VWO_ERR_TOO_LARGE;
     if (boundary == VWO_PERIODIC) {
+        #pragma omp parallel for schedule(static) if (n >= 32768)
         for (int t = 0; t < n; t++) {
             double sum = 0.0;
             for (int l = 0; l < fl; l++) sum += lo[l] * a[(t + l) % n];
@@ -423,6 +433,7 @@ static int apply_scaled_inverse(const double *a, const double *d, int n, const d
             y[t] = sum;
         }
     } else if (boundary == VWO_ZERO_PADDING) {
+        #pragma omp parallel for schedule(static) if (n >= 32768)
         for (int t = 0; t < n; t++) {
             double sum = 0.0;
             for (int l = 0; l < fl; l++) {
@@ -436,6 +447,7 @@ static int apply_scaled_inverse(const double *a, const double *d, int n, const d
         vwo_sym_decide(wavelet_id, L, level, &ap, &dh, &dp, &dg);
         int tauH = vwo_compute_tau(L, level) + dh;
         int tauG = vwo_compute_tau(L, level) + dg;
+        #pragma omp parallel for schedule(static) if (n >= 32768)
         for (int t = 0; t < n; t++) {
             double sum = 0.0;
             if (ap) { for (int l = 0; l < fl; l++) sum += lo[l] * a[vwo_symmetric_index(t + l - tauH, n)]; }
@@ -571,6 +583,7 @@ void vwo_swt_reconstruct_periodic(const double *details, const double *approx, i
         const double *det = details + (size_t)(level - 1) * n;
         int Lh = vwo_upsample_scale(lo, L, level, h);
         int Lg = vwo_upsample_scale(hi, L, level, g);
+        #pragma omp parallel for schedule(static) if (n >= 32768)
         for (int t = 0; t < n; t++) {
             double sum = 0.0;
             for (int l = 0; l < Lh; l++) sum += h[l] * cur[(t + l) % n];

@@ -1,0 +1,157 @@
+"""GPU parity at the BASELINE.json config shapes themselves (through the C ABI, vs the CPU restatement).
+
+  config 1  Haar MODWT level-1 PERIODIC, N = 1024                 MODWTTransform.java:131-299
+  config 3  sym8 SWT J=8 + universal soft-threshold denoise, N = 16384
+            (VectorWaveSwtAdapter.denoise :546-574: forward -> sigma = MAD(d_1)/0.6745 ->
+             T = sigma*sqrt(2 ln N) soft on every detail level -> reconstructPeriodic)
+  config 4  db8 MODWT J=10 on a 2^20-sample PERIODIC block, BatchMODWT semantics (no level cap,
+            BatchMODWT.java:90-111 / BatchSIMDMODWT.java:343-424; inverse = core reconstruct per signal,
+            BatchMODWT.java:151-178) -- exercises k_forward_multi, the column sweeps and k_inverse_multi
+  config 5  coif5 MODWT J=6 fp32, N = 8192 (no fp32 path in the reference: compared with the fp64
+            restatement at a relative tolerance)
+
+Bar: bit-exact (max-abs 0) in EXACT mode, thresholds equal; FMA within 1e-12 * max|x| (north_star).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+import vectorwave_amd as vw
+from vectorwave_amd.wavelets import Coiflet, Daubechies, Haar, Symlet
+
+pytestmark = pytest.mark.gpu
+
+
+def lohi(w):
+    return w.lowPassDecomposition(), w.highPassDecomposition()
+
+
+def exact(a, b, what=""):
+    a, b = np.asarray(a), np.asarray(b)
+    assert a.shape == b.shape, what
+    if not np.array_equal(a, b):
+        i = np.unravel_index(np.argmax(np.abs(a - b)), a.shape)
+        raise AssertionError(f"{what} not bit-exact: max |diff| = {np.max(np.abs(a - b)):.3e} at {i}")
+
+
+def config3_signals(B, n, seed=42):
+    """SURVEY.md §8d config 3 input: sin(2pi 3i/N) + 0.5 sin(2pi 37i/N) + 0.2 z, z Box-Muller of counter u."""
+    i = np.arange(n)
+    base = np.sin(2 * np.pi * 3 * i / n) + 0.5 * np.sin(2 * np.pi * 37 * i / n)
+    out = np.empty((B, n))
+    for b in range(B):
+        u1 = O.fill_uniform(n, seed, offset=(2 * b) * n) * 0.5 + 0.5      # (x+1)/2 in [0,1)
+        u2 = O.fill_uniform(n, seed, offset=(2 * b + 1) * n) * 0.5 + 0.5
+        z = np.sqrt(-2.0 * np.log1p(-u1)) * np.cos(2 * np.pi * u2)
+        out[b] = base + 0.2 * z
+    return out
+
+
+def test_config1_haar_level1_n1024(engine):
+    w = Haar.INSTANCE
+    x = O.fill_uniform(1024, 42)
+    tx = vw.MODWTTransform(w, vw.BoundaryMode.PERIODIC)
+    r = tx.forward(x)
+    a_ref, d_ref = O.modwt_forward(x, *lohi(w), O.PERIODIC)
+    exact(r.approximationCoeffs(), a_ref, "approx")
+    exact(r.detailCoeffs(), d_ref, "detail")
+    y = tx.inverse(r)
+    exact(y, O.modwt_inverse(a_ref, d_ref, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC), "y")
+    # the reference's own known answer (MODWTPercivalWaldenValidationTest.java:73)
+    r4 = tx.forward(np.array([1.0, 2.0, 3.0, 4.0]))
+    np.testing.assert_allclose(r4.approximationCoeffs(), [2.5, 1.5, 2.5, 3.5], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("fma", [False, True], ids=["exact", "fma"])
+def test_config3_sym8_swt_j8_denoise_16384(engine, fma):
+    w = Symlet.SYM8
+    n, J, B = 16384, 8, 4
+    x = config3_signals(B, n)
+    swt = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC, fma=fma)
+    y, thr = swt.denoise(x, J, return_thresholds=True)   # threshold < 0: universal, soft
+    for b in range(B):
+        y_ref, t_ref = O.swt_denoise(x[b], *lohi(w), O.PERIODIC, J, -1.0, True, wavelet_id=w.wavelet_id)
+        if fma:
+            assert abs(thr[b] - t_ref) <= 1e-12 * abs(t_ref)
+            np.testing.assert_allclose(y[b], y_ref, rtol=0, atol=1e-12 * np.max(np.abs(x[b])))
+        else:
+            assert thr[b] == t_ref, (b, thr[b], t_ref)
+            exact(y[b], y_ref, f"denoised signal {b}")
+
+
+def test_config3_device_tensors_batch(engine):
+    # the same pipeline on device-resident tensors (the bench path), 8 signals, EXACT
+    import torch
+    w = Symlet.SYM8
+    n, J, B = 16384, 8, 8
+    x = config3_signals(B, n, seed=7)
+    xd = torch.from_numpy(x).cuda()
+    y, thr = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC).denoise(xd, J, return_thresholds=True)
+    y, thr = y.cpu().numpy(), thr.cpu().numpy()
+    for b in (0, 5, 7):
+        y_ref, t_ref = O.swt_denoise(x[b], *lohi(w), O.PERIODIC, J, wavelet_id=w.wavelet_id)
+        assert thr[b] == t_ref
+        exact(y[b], y_ref, f"signal {b}")
+
+
+def test_config4_db8_j10_block_2p20(engine):
+    w = Daubechies.DB8
+    n, J = 1 << 20, 10
+    x = O.fill_uniform(n, 42).reshape(1, n)
+    m = vw.BatchMODWT.multiLevelAoS(w, x, J)
+    d_ref, a_ref = O.decompose(x[0], *lohi(w), O.PERIODIC, J, core=False)
+    for j in range(J):
+        exact(m.detailPerLevel[j, 0], d_ref[j], f"detail level {j + 1}")
+    exact(m.finalApprox[0], a_ref, "approximation")
+    y = vw.BatchMODWT.inverseMultiLevelAoS(w, m.detailPerLevel, m.finalApprox)
+    y_ref = O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC,
+                          w.wavelet_id)
+    exact(y[0], y_ref, "inverse")
+    # FMA mode on the same block: within the north_star tolerance of the exact result
+    mf = vw.BatchMODWT.multiLevelAoS(w, x, J, fma=True)
+    for j in range(J):
+        np.testing.assert_allclose(mf.detailPerLevel[j, 0], d_ref[j], rtol=0, atol=1e-12)
+    yf = vw.BatchMODWT.inverseMultiLevelAoS(w, mf.detailPerLevel, mf.finalApprox, fma=True)
+    np.testing.assert_allclose(yf[0], y_ref, rtol=0, atol=1e-12)
+
+
+def test_config4_streaming_blocks_independent(engine):
+    # BatchStreamingMODWT PERIODIC: every 2^20 block is an independent transform (BatchStreamingMODWT
+    # .java:110-116); two blocks of a 2-signal batch, second block compared level by level
+    import torch
+    w = Daubechies.DB8
+    n, J = 1 << 20, 10
+    s = vw.BatchStreamingMODWT(w, vw.BoundaryMode.PERIODIC, J)
+    blocks = [O.fill_uniform(2 * n, 42, offset=k * 2 * n).reshape(2, n) for k in range(2)]
+    for k, blk in enumerate(blocks):
+        r = s.processMultiLevel(torch.from_numpy(blk).cuda())
+    det = r.detailPerLevel.cpu().numpy()
+    for b in (1,):
+        d_ref, a_ref = O.decompose(blocks[1][b], *lohi(w), O.PERIODIC, J, core=False)
+        exact(det[:, b, :], d_ref, "block 2 details")
+        exact(r.finalApprox[b].cpu().numpy(), a_ref, "block 2 approximation")
+
+
+def test_config5_coif5_f32_j6_8192(engine):
+    import torch
+    w = Coiflet.COIF5
+    n, J, B = 8192, 6, 64
+    x64 = O.fill_uniform(B * n, 42).reshape(B, n)
+    x32 = x64.astype(np.float32)
+    xd = torch.from_numpy(x32).cuda()
+    tx = vw.MultiLevelMODWTTransform(w, vw.BoundaryMode.PERIODIC, fma=True)
+    res = tx.decompose(xd, J)
+    y = tx.reconstruct(res).cpu().numpy()
+    det, app = res.details_array.cpu().numpy(), res.approximation_array.cpu().numpy()
+    assert det.dtype == np.float32 and y.dtype == np.float32
+    tol = 2e-5 * J  # relative to max|x| = 1: fp32 rounding through J levels of 30-tap sums
+    for b in range(0, B, 9):
+        xr = x32[b].astype(np.float64)
+        d_ref, a_ref = O.decompose(xr, *lohi(w), O.PERIODIC, J)
+        np.testing.assert_allclose(det[:, b, :], d_ref, rtol=0, atol=tol)
+        np.testing.assert_allclose(app[b], a_ref, rtol=0, atol=tol)
+        y_ref = O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC)
+        np.testing.assert_allclose(y[b], y_ref, rtol=0, atol=tol)
+    assert np.max(np.abs(y - x32)) < 1e-3  # coif5's truncated taps + fp32

@@ -1,0 +1,103 @@
+"""Captured steps (vw_capture_begin / vw_capture_end / vw_graph_launch) and dtype safety of the
+device entry points.  A recorded graph replays exactly the calls it recorded: outputs are
+bit-identical to direct calls; calls that must synchronize are refused while capturing."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+import vectorwave_amd as vw
+from vectorwave_amd import _native as nat
+from vectorwave_amd.errors import InvalidStateException
+from vectorwave_amd.wavelets import Daubechies, Symlet
+
+pytestmark = pytest.mark.gpu
+
+
+def _bufs(torch, B, N, J, dt=None):
+    dt = dt or torch.float64
+    x = torch.empty((B, N), dtype=dt, device="cuda")
+    return x, torch.empty((J, B, N), dtype=dt, device="cuda"), torch.empty((B, N), dtype=dt, device="cuda"), \
+        torch.empty((B, N), dtype=dt, device="cuda")
+
+
+@pytest.mark.parametrize("w,B,N,J", [(Daubechies.DB4, 64, 4096, 6), (Daubechies.DB8, 2, 1 << 16, 8)],
+                         ids=["fused", "multilevel-tiles"])
+def test_graph_replay_bit_identical(engine, w, B, N, J):
+    import torch
+    from ctypes import c_void_p
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        x, det, app, y = _bufs(torch, B, N, J)
+        engine.fill_uniform(x, 42)
+        lo, hi = nat.taps_array(w.lowPassDecomposition()), nat.taps_array(w.highPassDecomposition())
+        lib, ctx = engine.lib, engine.ctx
+        P = lambda t: c_void_p(t.data_ptr())  # noqa: E731
+
+        def step():
+            assert lib.vw_modwt_forward_f64(ctx, P(x), B, N, N, lo, hi, len(lo), w.wavelet_id, 0, J, 0,
+                                            P(det), P(app)) == 0
+            assert lib.vw_modwt_inverse_f64(ctx, P(det), P(app), B, N, lo, hi, len(lo), w.wavelet_id, 0, J,
+                                            0xFFFFFFFF, 0, 0, P(y)) == 0
+
+        step()
+        torch.cuda.synchronize()
+        d0, a0, y0 = det.clone(), app.clone(), y.clone()
+        g = engine.capture(step)
+        for t in (det, app, y):
+            t.fill_(float("nan"))
+        g.launch(3)
+        torch.cuda.synchronize()
+        assert torch.equal(det, d0) and torch.equal(app, a0) and torch.equal(y, y0)
+        g.close()
+    xh = x.cpu().numpy()
+    d_ref, a_ref = O.decompose(xh[B - 1], w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC, J,
+                               core=False)
+    assert np.array_equal(d0[:, B - 1].cpu().numpy(), d_ref)
+    assert np.array_equal(a0[B - 1].cpu().numpy(), a_ref)
+
+
+def test_capture_refuses_synchronizing_calls(engine):
+    import torch
+    from ctypes import byref, c_void_p
+    w = Daubechies.DB4
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        x, det, app, _ = _bufs(torch, 4, 512, 3)
+        engine.bind_torch_stream()
+        lo, hi = nat.taps_array(w.lowPassDecomposition()), nat.taps_array(w.highPassDecomposition())
+        lib, ctx = engine.lib, engine.ctx
+        assert lib.vw_capture_begin(ctx) == 0
+        st = lib.vw_modwt_forward_f64(ctx, c_void_p(x.data_ptr()), 4, 512, 512, lo, hi, len(lo), w.wavelet_id, 0, 3,
+                                      nat.FLAG_VALIDATE, c_void_p(det.data_ptr()), c_void_p(app.data_ptr()))
+        assert st == 10  # VW_ERR_STATE
+        assert lib.vw_capture_begin(ctx) == 10  # already capturing
+        g = c_void_p()
+        assert lib.vw_capture_end(ctx, byref(g)) == 0
+        assert lib.vw_graph_destroy(g) == 0
+    # the null stream cannot be captured
+    engine.bind_torch_stream()
+    if torch.cuda.current_stream().cuda_stream == 0:
+        with pytest.raises(InvalidStateException):
+            engine.capture(lambda: None)
+
+
+def test_f32_tensor_into_f64_only_entry_points(engine):
+    # the f64-only entry points convert an f32 tensor instead of reading it as f64
+    import torch
+    w = Symlet.SYM8
+    x64 = torch.from_numpy(O.fill_uniform(2 * 2048, 42).reshape(2, 2048)).cuda()
+    x32 = x64.float()
+    ref = x32.double()
+    swt = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC)
+    assert torch.equal(swt.denoise(x32, 4), swt.denoise(ref, 4))
+    assert torch.equal(swt.estimateNoiseSigma(x32), swt.estimateNoiseSigma(ref))
+    tx = vw.MODWTTransform(w, vw.BoundaryMode.PERIODIC)
+    r32, r64 = tx.forward(x32[0]), tx.forward(ref[0])
+    assert torch.equal(r32.approximationCoeffs(), r64.approximationCoeffs())
+    # threshold_inplace on a non-contiguous view writes back in place
+    c = torch.from_numpy(O.fill_uniform(4 * 64, 7).reshape(64, 4)).cuda().t()  # [4, 64], non-contiguous
+    expect = c.clone().contiguous()
+    thr = torch.full((4,), 0.3, dtype=torch.float64, device="cuda")
+    engine.threshold_inplace(expect, thr, True)
+    engine.threshold_inplace(c, thr, True)
+    assert torch.equal(c, expect)

@@ -74,6 +74,10 @@ SIGNATURES = {
     "vw_ctx_enable_timing": (c_int, [c_void_p, c_int]),
     "vw_ctx_kernel_time": (c_int, [c_void_p, c_char_p, POINTER(c_double), POINTER(c_int64)]),
     "vw_ctx_reset_timing": (c_int, [c_void_p]),
+    "vw_capture_begin": (c_int, [c_void_p]),
+    "vw_capture_end": (c_int, [c_void_p, POINTER(c_void_p)]),
+    "vw_graph_launch": (c_int, [c_void_p, c_int64]),
+    "vw_graph_destroy": (c_int, [c_void_p]),
 }
 
 _lib = None

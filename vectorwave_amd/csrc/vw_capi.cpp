@@ -46,16 +46,66 @@ static vw_status ok() {
     if (e_ != hipSuccess) return fail(VW_ERR_DEVICE, "%s: %s", #call, hipGetErrorString(e_)); \
   } while (0)
 
+#define VW_TRY(expr)                      \
+  do {                                    \
+    vw_status s_ = (expr);                \
+    if (s_ != VW_OK) return s_;           \
+  } while (0)
+
 // ------------------------------------------------------------------------------------------------
 struct TimedLaunch {
   std::string family;
   hipEvent_t start, stop;
 };
 
+// Tuning switches (A/B experiments, tools/ab_*.sh), read from the environment ONCE per context at
+// vw_ctx_create -- never per call: a transform call does no getenv.  Defaults are the measured best.
+struct Tuning {
+  int nv = 4;              // VW_NV: vectors per thread of the fused kernels (4 or 8)
+  bool fwd_persist = true; // VW_FWD_PERSIST=0: no persistent forward
+  int fwd_buf = 0;         // VW_FWD_BUF=1|2: force one / two forward level buffers (0 = policy)
+  bool force_tiled = false;// VW_FORCE_TILED: per-level path even when the fused kernels fit
+  int fwd_rev = 0, inv_rev = 0;  // VW_FWD_REV / VW_INV_REV: reverse workgroup -> signal walk
+  int fwd_tile = 0;        // VW_FWD_TILE: per-level forward tile (0 = default)
+  bool multi = true;       // VW_MULTI=0: one launch per level on the long-signal path
+  int multi_div = 4;       // VW_MULTI_DIV: reach bound of a level group = tile / div
+  int multi_tile = 0;      // VW_MULTI_TILE: multi-level tile (0 = 16 KiB of samples)
+  int inv_buf = 0;         // VW_INV_BUF=2: two-buffer sequential inverse (k_inverse_db)
+  int inv_tile = 0;        // VW_INV_TILE: per-level inverse tile (0 = 1024)
+  int multi_rblk = 1;      // VW_MULTI_RBLK: register-blocked taps in k_inverse_multi
+  bool no_sweep = false;   // VW_NO_SWEEP: no column sweeps for deep levels
+  int sweep_qc = kSweepChunk;  // VW_SWEEP_QC: q-chunk per sweep thread
+};
+
+static Tuning read_tuning() {
+  Tuning t;
+  auto iv = [](const char* k, int def) { const char* e = getenv(k); return e ? atoi(e) : def; };
+  t.nv = iv("VW_NV", 4) <= 4 ? 4 : 8;
+  t.fwd_persist = iv("VW_FWD_PERSIST", 1) != 0;
+  t.fwd_buf = iv("VW_FWD_BUF", 0);
+  t.force_tiled = getenv("VW_FORCE_TILED") != nullptr;
+  t.fwd_rev = iv("VW_FWD_REV", 0);
+  t.inv_rev = iv("VW_INV_REV", 0);
+  t.fwd_tile = iv("VW_FWD_TILE", 0);
+  t.multi = iv("VW_MULTI", 1) != 0;
+  t.multi_div = std::max(1, iv("VW_MULTI_DIV", 4));
+  t.multi_tile = iv("VW_MULTI_TILE", 0);
+  t.inv_buf = iv("VW_INV_BUF", 0);
+  t.inv_tile = iv("VW_INV_TILE", 0);
+  t.multi_rblk = iv("VW_MULTI_RBLK", 1);
+  t.no_sweep = getenv("VW_NO_SWEEP") != nullptr;
+  const int qc = iv("VW_SWEEP_QC", kSweepChunk);
+  t.sweep_qc = qc >= 16 ? qc : kSweepChunk;
+  return t;
+}
+
 struct vw_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
+  bool capturing = false;      // between vw_capture_begin / vw_capture_end
+  unsigned ws_gen = 0;         // bumped when ws / ws2 move: graphs recorded before are stale
+  Tuning tune;
   std::recursive_mutex mu;
   void* ws = nullptr;          // tiled-path ping-pong buffers
   size_t ws_bytes = 0;
@@ -96,7 +146,7 @@ struct LaunchTimer {
   vw_ctx* c;
   TimedLaunch tl;
   bool on;
-  LaunchTimer(vw_ctx* ctx, const char* family) : c(ctx), on(ctx->timing) {
+  LaunchTimer(vw_ctx* ctx, const char* family) : c(ctx), on(ctx->timing && !ctx->capturing) {
     if (!on) return;
     tl.family = family;
     tl.start = pool_event(c);
@@ -127,8 +177,11 @@ static void collect_timing(vw_ctx* c) {
 
 static vw_status ensure_ws(vw_ctx* c, size_t bytes) {
   if (bytes <= c->ws_bytes) return VW_OK;
+  if (c->capturing) return fail(VW_ERR_STATE, "workspace growth during capture: run the call once before capturing it");
   if (c->ws) {
-    hipStreamSynchronize(c->stream);
+    // the workspace may have been used on streams the context was bound to before: drain the device
+    hipDeviceSynchronize();
+    ++c->ws_gen;
     hipFree(c->ws);
     c->ws = nullptr;
     c->ws_bytes = 0;
@@ -241,6 +294,7 @@ extern "C" vw_status vw_ctx_create(int device, vw_ctx** out) {
   VW_HIP(hipSetDevice(device));
   vw_ctx* c = new vw_ctx();
   c->device = device;
+  c->tune = read_tuning();
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(VW_ERR_DEVICE, "hipStreamCreate failed");
@@ -271,16 +325,35 @@ extern "C" vw_status vw_ctx_destroy(vw_ctx* c) {
 
 // The device's null (legacy default) stream -- what torch uses when no stream is set: its handle is
 // 0, which vw_ctx_set_stream reads as "own stream".
+// Rebinding the context: work already enqueued on the old stream (it may still use the shared
+// workspaces ws / ws2) is ordered before anything the new stream runs -- an event on the old stream
+// that the new one waits for.  An owned stream is drained and destroyed instead.
+static vw_status rebind_stream(vw_ctx* c, hipStream_t next, bool own_next) {
+  if (c->capturing) return fail(VW_ERR_STATE, "stream change during capture");
+  hipStream_t prev = c->stream;
+  if (c->own_stream) {
+    VW_HIP(hipStreamSynchronize(prev));
+    VW_HIP(hipStreamDestroy(prev));
+    c->own_stream = false;
+  } else if (prev != next) {
+    hipEvent_t ev = nullptr;
+    VW_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(ev, prev);
+    if (e == hipSuccess && next) e = hipStreamWaitEvent(next, ev, 0);
+    if (e == hipSuccess && !next) e = hipEventSynchronize(ev);  // the legacy null stream: drain
+    hipEventDestroy(ev);
+    if (e != hipSuccess) return fail(VW_ERR_DEVICE, "stream ordering failed: %s", hipGetErrorString(e));
+  }
+  c->stream = next;
+  c->own_stream = own_next;
+  return VW_OK;
+}
+
 extern "C" vw_status vw_ctx_use_null_stream(vw_ctx* c) {
   if (!c) return fail(VW_ERR_NULL, "ctx is null");
   std::lock_guard<std::recursive_mutex> g(c->mu);
   hipSetDevice(c->device);
-  if (c->own_stream) {
-    hipStreamSynchronize(c->stream);
-    hipStreamDestroy(c->stream);
-    c->own_stream = false;
-  }
-  c->stream = nullptr;
+  VW_TRY(rebind_stream(c, nullptr, false));
   return ok();
 }
 
@@ -288,18 +361,81 @@ extern "C" vw_status vw_ctx_set_stream(vw_ctx* c, void* s) {
   if (!c) return fail(VW_ERR_NULL, "ctx is null");
   std::lock_guard<std::recursive_mutex> g(c->mu);
   hipSetDevice(c->device);
-  if (c->own_stream) {
-    hipStreamSynchronize(c->stream);
-    hipStreamDestroy(c->stream);
-    c->own_stream = false;
-    c->stream = nullptr;
-  }
   if (s) {
-    c->stream = (hipStream_t)s;
+    VW_TRY(rebind_stream(c, (hipStream_t)s, false));
   } else {
-    VW_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    c->own_stream = true;
+    hipStream_t ns = nullptr;
+    VW_HIP(hipStreamCreateWithFlags(&ns, hipStreamNonBlocking));
+    VW_TRY(rebind_stream(c, ns, true));
   }
+  return ok();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Captured steps: the calls made between vw_capture_begin and vw_capture_end are recorded (stream
+// capture of the context stream) into one executable HIP graph, replayed by vw_graph_launch with
+// one host call -- the host-side planning, argument packing and per-kernel launch cost of the
+// transforms are paid once at capture.  Calls that must synchronize (validation, host memory,
+// SYNC, workspace growth) are rejected while capturing.
+struct vw_graph {
+  vw_ctx* ctx = nullptr;
+  unsigned ws_gen = 0;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+};
+
+extern "C" vw_status vw_capture_begin(vw_ctx* c) {
+  if (!c) return fail(VW_ERR_NULL, "ctx is null");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (c->capturing) return fail(VW_ERR_STATE, "already capturing");
+  if (!c->stream) return fail(VW_ERR_STATE, "the null stream cannot be captured; bind a stream first");
+  hipSetDevice(c->device);
+  VW_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
+  c->capturing = true;
+  return ok();
+}
+
+extern "C" vw_status vw_capture_end(vw_ctx* c, vw_graph** out) {
+  if (!c || !out) return fail(VW_ERR_NULL, "null argument");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (!c->capturing) return fail(VW_ERR_STATE, "not capturing");
+  hipSetDevice(c->device);
+  c->capturing = false;
+  hipGraph_t graph = nullptr;
+  VW_HIP(hipStreamEndCapture(c->stream, &graph));
+  hipGraphExec_t exec = nullptr;
+  hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
+  if (e != hipSuccess) {
+    hipGraphDestroy(graph);
+    return fail(VW_ERR_DEVICE, "graph instantiate failed: %s", hipGetErrorString(e));
+  }
+  vw_graph* gr = new vw_graph();
+  gr->ctx = c;
+  gr->ws_gen = c->ws_gen;
+  gr->graph = graph;
+  gr->exec = exec;
+  *out = gr;
+  return ok();
+}
+
+extern "C" vw_status vw_graph_launch(vw_graph* gr, int64_t count) {
+  if (!gr) return fail(VW_ERR_NULL, "graph is null");
+  vw_ctx* c = gr->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (gr->ws_gen != c->ws_gen)
+    return fail(VW_ERR_STATE, "the context workspace moved since this graph was recorded; record it again");
+  hipSetDevice(c->device);
+  for (int64_t i = 0; i < count; ++i) VW_HIP(hipGraphLaunch(gr->exec, c->stream));
+  return ok();
+}
+
+extern "C" vw_status vw_graph_destroy(vw_graph* gr) {
+  if (!gr) return fail(VW_ERR_NULL, "graph is null");
+  hipSetDevice(gr->ctx->device);
+  hipStreamSynchronize(gr->ctx->stream);
+  if (gr->exec) hipGraphExecDestroy(gr->exec);
+  if (gr->graph) hipGraphDestroy(gr->graph);
+  delete gr;
   return ok();
 }
 
@@ -381,6 +517,13 @@ static void copy_taps(T* dst, const double* src, int L) {
   for (int i = L; i < kMaxTaps; ++i) dst[i] = T(0);
 }
 
+// Calls that synchronize cannot be recorded into a graph (vw_capture_begin).
+static vw_status capture_guard(vw_ctx* c, unsigned flags) {
+  if (c->capturing && (flags & (VW_FLAG_VALIDATE | VW_FLAG_HOST_MEMORY | VW_FLAG_SYNC)))
+    return fail(VW_ERR_STATE, "validation, host memory and SYNC cannot be captured");
+  return VW_OK;
+}
+
 static vw_status read_bad(vw_ctx* c, unsigned long long* out) {
   VW_HIP(hipMemcpyAsync(out, c->bad, sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
   VW_HIP(hipStreamSynchronize(c->stream));
@@ -402,11 +545,10 @@ static vw_status report_bad(unsigned long long bad, int64_t N) {
 // ceil(nvec / NV) threads (not rounded to a wave): thread `tid` owns vectors tid + k*threads, and
 // the unrolled kernels rely on slabs 0..NV-2 being full, `fit` = (NV-1)*threads <= nvec (else the
 // runtime-L kernel with a bounds check per vector runs).
-static bool fused_plan(int64_t N, int V, int elem, int64_t lds_elems_extra, int* threads, int* nv, int* lds,
-                       bool* fit) {
+static bool fused_plan(const Tuning& tu, int64_t N, int V, int elem, int64_t lds_elems_extra, int* threads, int* nv,
+                       int* lds, bool* fit) {
   const int64_t nvec = (N + V - 1) / V;
-  int want = 4;
-  if (const char* e = getenv("VW_NV")) want = atoi(e) <= 4 ? 4 : 8;
+  int want = tu.nv;
   if ((nvec + want - 1) / want > 512) want = 8;  // NV = 4 kernels are bounded to 512 threads (VW_FUSED_BOUNDS)
   const int64_t th = (nvec + want - 1) / want;
   if (th > kMaxThreads) return false;
@@ -419,15 +561,6 @@ static bool fused_plan(int64_t N, int V, int elem, int64_t lds_elems_extra, int*
   return true;
 }
 
-// q-chunk per column-sweep thread (VW_SWEEP_QC overrides, for tuning)
-static int sweep_chunk() {
-  static const int qc = [] {
-    const char* e = getenv("VW_SWEEP_QC");
-    const int v = e ? atoi(e) : kSweepChunk;
-    return v >= 16 ? v : kSweepChunk;
-  }();
-  return qc;
-}
 
 // Owner-written halo of one level (vw_device.h halo_images): the affine images of an element and
 // the vector bands that have them; `own` only when every band lies in the slab that checks it.
@@ -462,19 +595,17 @@ static void set_halo_images(LevelDesc& d, int64_t N, int64_t npow2, int V, int t
 // of the group starting at level j (0 inside a group, 1 = the per-level kernels).  VW_MULTI=0
 // disables; VW_MULTI_TILE / VW_MULTI_DIV tune tile and reach bound.
 template <typename T>
-static int multi_tile() {
+static int multi_tile(const Tuning& tu) {
   constexpr int V = vec_width<T>();
-  const char* e = getenv("VW_MULTI_TILE");
-  const int v = e ? atoi(e) : (int)(16384 / sizeof(T));
+  const int v = tu.multi_tile ? tu.multi_tile : (int)(16384 / sizeof(T));
   return v >= 64 * V ? v / V * V : 64 * V;
 }
 
-static std::vector<int> level_groups(const std::vector<LevelDesc>& lv, int J, int L, int V, int tile, bool ok) {
+static std::vector<int> level_groups(const Tuning& tu, const std::vector<LevelDesc>& lv, int J, int L, int V, int tile,
+                                     bool ok) {
   std::vector<int> g(J, 1);
-  const char* en = getenv("VW_MULTI");
-  if (!ok || (en && atoi(en) == 0)) return g;
-  const char* dv = getenv("VW_MULTI_DIV");
-  const int64_t cap = tile / std::max(1, dv ? atoi(dv) : 4);
+  if (!ok || !tu.multi) return g;
+  const int64_t cap = tile / tu.multi_div;
   for (int j = 1; j <= J;) {
     int n = 0;
     int64_t ext = 0;
@@ -502,11 +633,10 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
                               const double* hi, int L, int boundary, int J, unsigned flags, T* details, T* approx,
                               bool single_level, int mode_override, T* const* hist, bool hist_update) {
   constexpr int V = vec_width<T>();
+  VW_TRY(capture_guard(c, flags));
   const bool fma = flags & VW_FLAG_FMA;
   const bool validate = flags & VW_FLAG_VALIDATE;
   const int64_t nvec = (N + V - 1) / V;
-  const int tmax = (int)(nvec * V - 1);
-  (void)tmax;
 
   std::vector<LevelDesc> lv(J);
   int max_hl = 0;
@@ -543,21 +673,20 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
   // Persistent variant (vw_device.h k_forward_persist): next row by LDS-DMA during the last level.
   // Its contract: two buffers, full slabs of whole waves, rows in 64-vector chunks, no validation
   // or streaming history.  VW_FWD_PERSIST=0 disables it.
-  const char* pe = getenv("VW_FWD_PERSIST");
-  const bool persist_on = !pe || atoi(pe) != 0;
+  const Tuning& tu = c->tune;
+  const bool persist_on = tu.fwd_persist;
   const bool io_aligned = (ldx % V == 0) && (N % V == 0) && aligned16(x) && aligned16(details) && aligned16(approx);
   auto persist_ok = [&](int th, int nvv, bool ft) {
     return persist_on && io_aligned && ft && nvv == 4 && !validate && !hist && (int64_t)th * nvv == nvec &&
            th % 64 == 0 && nvec % 64 == 0 && has_unrolled_taps(L) && J >= 1;
   };
   const int64_t region = round_up(hlpad + nvec * V + V, V);
-  const char* fb = getenv("VW_FWD_BUF");
-  bool dbl = fb ? atoi(fb) == 2 : true;
+  bool dbl = tu.fwd_buf ? tu.fwd_buf == 2 : true;
   bool fused = false, fit = false;
-  if (J <= kMaxLevels && !getenv("VW_FORCE_TILED")) {
-    if (dbl) dbl = fused_plan(N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
-    if (dbl && !fb && !fma && !persist_ok(threads, nv, fit)) dbl = false;  // EXACT without persistence
-    fused = dbl || fused_plan(N, V, sizeof(T), region, &threads, &nv, &lds, &fit);
+  if (J <= kMaxLevels && !tu.force_tiled) {
+    if (dbl) dbl = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
+    if (dbl && !tu.fwd_buf && !fma && !persist_ok(threads, nv, fit)) dbl = false;  // EXACT without persistence
+    fused = dbl || fused_plan(tu, N, V, sizeof(T), region, &threads, &nv, &lds, &fit);
   }
   if (fused) {
     for (int j = 0; j < J; ++j) set_halo_images(lv[j], N, npow2, V, threads, nv);
@@ -568,7 +697,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     a.vec_io = (ldx % V == 0) && (N % V == 0) && aligned16(x) && aligned16(details) && aligned16(approx);
     a.unrolled = a.vec_io && fit;
     a.validate = validate; a.bad = c->bad;
-    a.rev = getenv("VW_FWD_REV") ? atoi(getenv("VW_FWD_REV")) : 0;
+    a.rev = tu.fwd_rev;
     for (int j = 0; j < J; ++j) a.hist[j] = hist ? hist[j] : nullptr;
     a.hist_update = hist_update ? 1 : 0;
     a.taps = L;
@@ -588,7 +717,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     // Deep levels (s >= kSweepMinS) run as column sweeps, shallow ones as LDS tiles with a halo.
     for (int j = 1; hist && j <= J; ++j)
       if (lv[j - 1].hist_len > N) return fail(VW_ERR_UNSUPPORTED, "streaming block shorter than level %d history", j);
-    const int tile_max = getenv("VW_FWD_TILE") ? atoi(getenv("VW_FWD_TILE")) / V * V : 256 * kNV * V;
+    const int tile_max = tu.fwd_tile ? tu.fwd_tile / V * V : 256 * kNV * V;
     const size_t plane = (size_t)B * (size_t)N;
     const vw_status st = ensure_ws(c, 2 * plane * sizeof(T) + 256);
     if (st != VW_OK) return st;
@@ -596,8 +725,8 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     if (validate) VW_HIP(hipMemsetAsync(c->bad, 0xFF, sizeof(unsigned long long), c->stream));
     const T* src = x;
     int64_t lda = ldx;
-    const int mtile = multi_tile<T>();
-    const std::vector<int> groups = level_groups(lv, J, L, V, mtile, !validate && !hist);
+    const int mtile = multi_tile<T>(tu);
+    const std::vector<int> groups = level_groups(tu, lv, J, L, V, mtile, !validate && !hist);
     for (int j = 1; j <= J; ++j) {
       T* const nxt = (src == tmp[0]) ? tmp[1] : tmp[0];  // never the level's own input
       if (groups[j - 1] >= 2) {
@@ -648,12 +777,12 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
       a.validate = validate; a.bad = c->bad; a.npow2 = npow2; a.taps = L;
       copy_taps(a.lo, lo, L);
       copy_taps(a.hi, hi, L);
-      const bool sweep = a.lv.s >= kSweepMinS && has_unrolled_taps(L) && !getenv("VW_NO_SWEEP");
+      const bool sweep = a.lv.s >= kSweepMinS && has_unrolled_taps(L) && !tu.no_sweep;
       {
         LaunchTimer lt(c, "forward_level");
         hipError_t e;
         if (sweep) {
-          a.tile = sweep_chunk();
+          a.tile = tu.sweep_qc;
           e = launch_forward_sweep<T>(a, fma, c->stream);
         } else {
           e = launch_forward_level<T>(a, (int)(elems * sizeof(T)), fma, c->stream);
@@ -690,6 +819,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
                               int approx_zero, unsigned flags, T* y, bool single_level, const T* thr, int soft,
                               int64_t thr_ld = 0) {
   constexpr int V = vec_width<T>();
+  VW_TRY(capture_guard(c, flags));
   const bool fma = flags & VW_FLAG_FMA;
   const int64_t nvec = (N + V - 1) / V;
   const int tmax = (int)(nvec * V - 1);
@@ -730,14 +860,14 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   // (k_inverse_seq, four barriers per level) -- measured faster on MI355X than two buffers
   // (k_inverse_db, two barriers per level) because twice the workgroups fit per CU; VW_INV_BUF=2
   // selects the latter.
-  bool db = false;
-  if (const char* e = getenv("VW_INV_BUF")) db = !pair && atoi(e) == 2;
+  const Tuning& tu = c->tune;
+  bool db = !pair && tu.inv_buf == 2;
   bool fused = false, fit = false;
-  if (!getenv("VW_FORCE_TILED")) {
-    if (pair || db) fused = fused_plan(N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
+  if (!tu.force_tiled) {
+    if (pair || db) fused = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
     if (!fused && !pair) {
       db = false;
-      fused = fused_plan(N, V, sizeof(T), region, &threads, &nv, &lds, &fit);
+      fused = fused_plan(tu, N, V, sizeof(T), region, &threads, &nv, &lds, &fit);
     }
   }
   if (fused) {
@@ -750,7 +880,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     a.vec_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
     a.unrolled = a.vec_io && fit;
     a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.thr_ld = thr_ld; a.soft = soft; a.taps = L;
-    a.rev = getenv("VW_INV_REV") ? atoi(getenv("VW_INV_REV")) : 0;
+    a.rev = tu.inv_rev;
     copy_taps(a.lo, lo, L);
     copy_taps(a.hi, hi, L);
     for (int j = 0; j < J; ++j) a.lv[j] = lv[j];
@@ -763,15 +893,15 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   } else {
     // 1024-sample tiles: two LDS regions of ~9 KiB keep many workgroups per CU (measured best on
     // MI355X for db8 2^20-sample blocks; VW_INV_TILE overrides)
-    const int tile_max = getenv("VW_INV_TILE") ? atoi(getenv("VW_INV_TILE")) / V * V : 1024;
+    const int tile_max = tu.inv_tile ? tu.inv_tile / V * V : 1024;
     const size_t plane = (size_t)B * (size_t)N;
     const vw_status st = ensure_ws(c, 2 * plane * sizeof(T) + 256);
     if (st != VW_OK) return st;
     T* tmp[2] = {reinterpret_cast<T*>(c->ws), reinterpret_cast<T*>(c->ws) + plane};
     const T* cur = approx_zero ? nullptr : approx;
     // multi-level groups (PERIODIC sequential sums): start level of the group whose top is j
-    const int mtile = multi_tile<T>();
-    const std::vector<int> groups = level_groups(lv, J, L, V, mtile, !pair && boundary == VW_PERIODIC);
+    const int mtile = multi_tile<T>(tu);
+    const std::vector<int> groups = level_groups(tu, lv, J, L, V, mtile, !pair && boundary == VW_PERIODIC);
     std::vector<int> start_of(J + 1, 0);
     for (int j = 1; j <= J; ++j) {
       if (groups[j - 1] < 2) continue;
@@ -799,7 +929,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         m.region = (int)round_up(mtile + m.ext[g - 1] + V, V);
         m.vec_io = (N % V == 0) && al;
         m.soft = soft; m.taps = L;
-        { const char* rb = getenv("VW_MULTI_RBLK"); m.rblk = rb ? atoi(rb) : 1; }
+        m.rblk = tu.multi_rblk;
         copy_taps(m.lo, lo, L);
         copy_taps(m.hi, hi, L);
         LaunchTimer lt(c, "inverse_level");
@@ -828,8 +958,8 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       copy_taps(a.hi, hi, L);
       LaunchTimer lt(c, "inverse_level");
       hipError_t e;
-      if (a.lv.s >= kSweepMinS && has_unrolled_taps(L) && !getenv("VW_NO_SWEEP")) {
-        a.tile = sweep_chunk();
+      if (a.lv.s >= kSweepMinS && has_unrolled_taps(L) && !tu.no_sweep) {
+        a.tile = tu.sweep_qc;
         e = launch_inverse_sweep<T>(a, fma, c->stream);
       } else {
         e = launch_inverse_level<T>(a, (int)(2 * reg * sizeof(T)), fma, c->stream);
@@ -868,11 +998,6 @@ struct Staging {
   }
 };
 
-#define VW_TRY(expr)                      \
-  do {                                    \
-    vw_status s_ = (expr);                \
-    if (s_ != VW_OK) return s_;           \
-  } while (0)
 
 template <typename T>
 static vw_status modwt_forward(vw_ctx* c, const T* x, int64_t B, int64_t N, int64_t ldx, const double* lo,
@@ -1117,8 +1242,10 @@ static vw_status denoise_device(vw_ctx* c, const double* x, int64_t B, int64_t N
   // workspace: details [J][B][N] | approx [B][N] | thr [B]   (tiled levels use ws beyond, via a 2nd alloc)
   const size_t bytes = align_up(((size_t)J + 1) * plane * sizeof(double), 256) + align_up((size_t)B * 8, 256);
   if (bytes > c->ws2_bytes) {
+    if (c->capturing) return fail(VW_ERR_STATE, "workspace growth during capture: run the call once before capturing it");
     if (c->ws2) {
-      hipStreamSynchronize(c->stream);
+      hipDeviceSynchronize();
+      ++c->ws_gen;
       hipFree(c->ws2);
       c->ws2 = nullptr;
       c->ws2_bytes = 0;
@@ -1134,12 +1261,14 @@ static vw_status denoise_device(vw_ctx* c, const double* x, int64_t B, int64_t N
   vw_status st = forward_impl<double>(c, x, B, N, ldx, lo, hi, L, boundary, J, flags & ~VW_FLAG_SYNC, det, app, false,
                                       -1, nullptr, false);
   if (st == VW_OK) {
-    hipError_t e;
+    hipError_t e = hipSuccess;
     if (threshold < 0) {
       // T = sigma * Math.sqrt(2 * Math.log(n))  core/swt/VectorWaveSwtAdapter.java:514
       const double scale_c = std::sqrt(2 * std::log((double)N));
       LaunchTimer lt(c, "sigma");
       e = launch_noise_sigma(det, N, B, (int)N, scale_c, nullptr, thr, c->stream);
+    } else if (c->capturing) {
+      st = fail(VW_ERR_STATE, "a fixed threshold cannot be captured");
     } else {
       std::vector<double> h((size_t)B, threshold);
       e = hipMemcpyAsync(thr, h.data(), (size_t)B * sizeof(double), hipMemcpyHostToDevice, c->stream);
@@ -1199,8 +1328,10 @@ static vw_status wavelet_denoise_device(vw_ctx* c, const double* x, int64_t B, i
   const size_t coef_bytes = align_up(((size_t)J + 1) * plane * sizeof(double), 256);
   const size_t bytes = coef_bytes + align_up((size_t)B * 8, 256) + align_up((size_t)J * B * 8, 256);
   if (bytes > c->ws2_bytes) {
+    if (c->capturing) return fail(VW_ERR_STATE, "workspace growth during capture: run the call once before capturing it");
     if (c->ws2) {
-      hipStreamSynchronize(c->stream);
+      hipDeviceSynchronize();
+      ++c->ws_gen;
       hipFree(c->ws2);
       c->ws2 = nullptr;
       c->ws2_bytes = 0;
@@ -1220,6 +1351,7 @@ static vw_status wavelet_denoise_device(vw_ctx* c, const double* x, int64_t B, i
   if (st != VW_OK) return st;
   hipError_t e = hipSuccess;
   if (method == kThrFixed) {
+    if (c->capturing) return fail(VW_ERR_STATE, "a fixed threshold cannot be captured");
     std::vector<double> h((size_t)B, fixed);
     e = hipMemcpyAsync(thr, h.data(), (size_t)B * sizeof(double), hipMemcpyHostToDevice, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
@@ -1404,6 +1536,7 @@ extern "C" vw_status vw_stream_flush_f64(vw_stream* s, int64_t tail_len, unsigne
                 min_hist);
   if (!details || !approx) return fail(VW_ERR_NULL, "null output");
   std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (c->capturing) return fail(VW_ERR_STATE, "flush cannot be captured");
   hipSetDevice(c->device);
   const int64_t B = s->last_batch;
   const int h0 = s->hist_len[0];

@@ -1,30 +1,8 @@
-#define VW_T double
-// vw_fwd_f64.hip -- launchers (instantiation unit) for the kernels in vw_device.h.
-#include "vw_device.h"
+// vw_fwd.hip -- launchers (instantiation unit, once per element type) for the kernels in vw_device.h.
+#include "vw_launch.h"
 #include <algorithm>
 
 namespace vw {
-
-// Unrolled tap counts; other L use the runtime-L kernels.  Dev builds may restrict the list:
-// make DEV_TAPS='X(8)' (the runtime-L kernel still covers every other L).
-#ifdef VW_DEV_TAPS
-#define VW_TAP_LIST(X) VW_DEV_TAPS(X)
-#else
-#define VW_TAP_LIST(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(24) X(30)
-#endif
-
-// Raise the dynamic-LDS limit once per kernel instantiation (a call per launch costs host time).
-// `configured` must be a static of the caller, which is unique per kernel instantiation.
-template <typename Kern>
-static hipError_t set_lds(Kern k, int lds_bytes, int* configured) {
-  if (lds_bytes > *configured) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       kLdsBytes);
-    if (e != hipSuccess) return e;
-    *configured = kLdsBytes;
-  }
-  return hipSuccess;
-}
 
 template <typename T, int L, bool FMA, int NV>
 static hipError_t run_forward_fused_nv(const FwdArgs<T>& a, int threads, int lds, hipStream_t st) {
@@ -67,8 +45,14 @@ static hipError_t run_forward_persist(const FwdArgs<T>& a, int threads, int lds,
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
   }
-  int per_cu = 0;
-  if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds)) != hipSuccess) return e;
+  // resident workgroups per CU: one occupancy query per (threads, LDS) shape, not one per launch
+  static int q_threads = -1, q_lds = -1, q_per_cu = 0;
+  if (threads != q_threads || lds != q_lds) {
+    int per_cu = 0;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds)) != hipSuccess) return e;
+    q_threads = threads; q_lds = lds; q_per_cu = per_cu;
+  }
+  const int per_cu = q_per_cu;
   if (per_cu < 1) return hipErrorInvalidConfiguration;
   const long long grid = std::min<long long>(a.B, (long long)per_cu * cus);
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(threads), lds, st, a);

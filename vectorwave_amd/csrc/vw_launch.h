@@ -1,0 +1,33 @@
+// vw_launch.h -- shared by the launcher units vw_fwd.hip / vw_inv.hip / vw_lvl.hip, each compiled once
+// per element type (the Makefile passes -DVW_T=double or -DVW_T=float).
+#pragma once
+#include "vw_device.h"
+
+#ifndef VW_T
+#error "compile with -DVW_T=double or -DVW_T=float"
+#endif
+
+namespace vw {
+
+// Unrolled tap counts; other L use the runtime-L kernels.  Dev builds may restrict the list:
+// make DEV_TAPS='X(8)' (the runtime-L kernel still covers every other L).
+#ifdef VW_DEV_TAPS
+#define VW_TAP_LIST(X) VW_DEV_TAPS(X)
+#else
+#define VW_TAP_LIST(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(24) X(30)
+#endif
+
+// Raise the dynamic-LDS limit once per kernel instantiation (a call per launch costs host time).
+// `configured` must be a static of the caller, which is unique per kernel instantiation.
+template <typename Kern>
+static hipError_t set_lds(Kern k, int lds_bytes, int* configured) {
+  if (lds_bytes > *configured) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       kLdsBytes);
+    if (e != hipSuccess) return e;
+    *configured = kLdsBytes;
+  }
+  return hipSuccess;
+}
+
+}  // namespace vw

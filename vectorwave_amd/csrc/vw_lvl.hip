@@ -1,29 +1,7 @@
-#define VW_T float
-// vw_lvl_f32.hip -- launchers (instantiation unit) for the kernels in vw_device.h.
-#include "vw_device.h"
+// vw_lvl.hip -- launchers (instantiation unit, once per element type) for the kernels in vw_device.h.
+#include "vw_launch.h"
 
 namespace vw {
-
-// Unrolled tap counts; other L use the runtime-L kernels.  Dev builds may restrict the list:
-// make DEV_TAPS='X(8)' (the runtime-L kernel still covers every other L).
-#ifdef VW_DEV_TAPS
-#define VW_TAP_LIST(X) VW_DEV_TAPS(X)
-#else
-#define VW_TAP_LIST(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(24) X(30)
-#endif
-
-// Raise the dynamic-LDS limit once per kernel instantiation (a call per launch costs host time).
-// `configured` must be a static of the caller, which is unique per kernel instantiation.
-template <typename Kern>
-static hipError_t set_lds(Kern k, int lds_bytes, int* configured) {
-  if (lds_bytes > *configured) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       kLdsBytes);
-    if (e != hipSuccess) return e;
-    *configured = kLdsBytes;
-  }
-  return hipSuccess;
-}
 
 template <typename T, int L, bool FMA, bool INV>
 static hipError_t run_level(const LevelArgs<T>& a, int lds, hipStream_t st) {

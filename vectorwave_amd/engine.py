@@ -88,7 +88,13 @@ class Engine:
     def _prep(self, x, dtype=None):
         """Returns (array, is_device, ptr, dtype_is_f32)."""
         if _is_device_tensor(x):
-            if x.dtype not in (torch.float64, torch.float32):
+            # an f64-only entry point (dtype=float64) must never get an f32 buffer: the kernel would
+            # read and write 8-byte elements over a 4-byte allocation
+            if dtype is not None:
+                want = torch.float32 if np.dtype(dtype) == np.float32 else torch.float64
+                if x.dtype != want:
+                    x = x.to(want)
+            elif x.dtype not in (torch.float64, torch.float32):
                 x = x.to(torch.float64)
             if not x.is_contiguous():
                 x = x.contiguous()
@@ -224,9 +230,26 @@ class Engine:
         B, N = (1, ca.shape[0]) if one else ca.shape
         ta, _, tp, _ = self._prep(thresholds, np.float64)
         _check(self.lib.vw_threshold_f64(self.ctx, cp, B, N, tp, 1 if soft else 0, self._flags(0, dev)))
-        if not dev and ca is not coeffs:
-            np.copyto(coeffs, ca)
+        if ca is not coeffs:  # _prep made a converted / contiguous copy: write the result back in place
+            if dev:
+                coeffs.copy_(ca)
+            else:
+                np.copyto(coeffs, ca)
         return coeffs
+
+    # -- captured steps (vw_capture_begin / vw_capture_end / vw_graph_launch) --------------------
+    def capture(self, fn) -> "Graph":
+        """Record the engine calls ``fn()`` makes (device tensors, no validation) into one HIP graph.
+        The engine must be bound to a non-default torch stream (``bind_torch_stream``)."""
+        self.bind_torch_stream()
+        _check(self.lib.vw_capture_begin(self.ctx))
+        try:
+            fn()
+        finally:
+            g = c_void_p()
+            st = self.lib.vw_capture_end(self.ctx, byref(g))
+        _check(st)
+        return Graph(self, g)
 
     def fill_uniform(self, x, seed: int, offset: int = 0):
         """Device generator of the bench input: x = 2u-1, u = (splitmix64(seed ^ (offset+i)) >> 11) 2^-53."""
@@ -236,6 +259,28 @@ class Engine:
         fn = self.lib.vw_fill_uniform_f32 if x.dtype == torch.float32 else self.lib.vw_fill_uniform_f64
         _check(fn(self.ctx, c_void_p(x.data_ptr()), x.numel(), ctypes.c_uint64(seed), offset))
         return x
+
+
+class Graph:
+    """An executable HIP graph of recorded engine calls; ``launch(count)`` replays it on the stream."""
+
+    def __init__(self, engine: Engine, handle: c_void_p):
+        self.engine = engine
+        self.handle = handle
+
+    def launch(self, count: int = 1) -> None:
+        _check(self.engine.lib.vw_graph_launch(self.handle, int(count)))
+
+    def close(self) -> None:
+        if self.handle:
+            _check(self.engine.lib.vw_graph_destroy(self.handle))
+            self.handle = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def version() -> str:
