@@ -7,10 +7,12 @@ scaling) -- no collective on the data path.  With N > 1 the same
 N = 1 (4096 rows per rank) is timed afterwards and reported as `weak_scaling`.
 
 A "step" = one multi-level forward pass + one multi-level inverse pass over the rank's rows, inputs
-already resident in HBM (generated on device by the counter-based generator).  Each pass is
-recorded once into a HIP graph through the C ABI (vw_capture_begin / vw_graph_launch): the timed
-loop replays the graphs, so host-side planning and kernel-argument packing are not on the clock --
-at 8 GPUs a pass is ~30 us of GPU work.
+already resident in HBM (generated on device by the counter-based generator).  The K timed steps are
+recorded once through the C ABI into one HIP graph (vw_capture_begin / vw_graph_launch) and replayed
+once: no host-side planning or kernel-argument packing inside the timed region -- at 8 GPUs a pass is
+~30 us of GPU work.  Every kernel launch of those K steps is bracketed by HIP event nodes inside the
+graph, so per-kernel durations come from the timed steps themselves (`--launch direct|graph-step`
+and `--events none` for A/B).
 
 Clock settle: an MI355X leaving idle runs the first ~50 ms of load below its steady clock (measured
 per step, profiles/r02/trace_*.log).  Before the W warmup steps the step is replayed for
@@ -22,8 +24,7 @@ time is the max over ranks.
 MASTER_*) before any GPU call and relays rank 0's line.  Under torchrun each process is one rank.
 
 Prints ONE JSON line (rank 0) with value = Msamples/s of the whole job, a `roofline` object for the
-dominant pass (algorithmic bytes per launch / its average HIP-event duration, events recorded around
-every graph replay inside the timed loop) and a `cpu_baseline` object (the C restatement of
+dominant pass (algorithmic bytes per launch / its average HIP-event duration over the timed steps) and a `cpu_baseline` object (the C restatement of
 vectorwave-core's scalar loops, timed on a bounded sample on this host's cores, N = 1 only).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config db4|sym8-denoise|db8-stream|coif5-f32]
@@ -45,6 +46,12 @@ ACC_NAME = {
     False: "exact (separate multiply and add in the reference's tap order; bit-identical to vectorwave-core)",
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
+
+LAUNCH_DESC = {
+    "graph-k": "the K timed steps recorded once into one HIP graph (vw_capture_begin / vw_graph_launch), replayed once",
+    "graph-step": "a one-step HIP graph replayed K times",
+    "direct": "direct C-ABI calls",
+}
 
 # name: (wavelet, levels, GLOBAL batch, N, dtype, pipeline) -- BASELINE.json configs[1..4]
 CONFIGS = {
@@ -68,9 +75,10 @@ def parse(argv=None):
                    help="headline in EXACT accumulation (bit-identical to vectorwave-core) instead of FMA")
     p.add_argument("--no-alt", action="store_true", help="skip the timing of the other accumulation mode")
     p.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling measurement")
-    p.add_argument("--no-graph", action="store_true", help="direct C-ABI calls in the timed loop instead of graphs")
+    p.add_argument("--launch", default="graph-k", choices=sorted(LAUNCH_DESC),
+                   help="how the timed steps are issued (see measure())")
     p.add_argument("--events", default="inline", choices=["inline", "none"],
-                   help="HIP events around every pass inside the timed loop (inline) or none")
+                   help="HIP events around every kernel launch inside the timed steps (inline) or none")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--dry-run", action="store_true",
@@ -196,20 +204,13 @@ class Workload:
             self.eng.ctx, xp, B, N, N, self.lo_a, self.hi_a, self.L, w.wavelet_id, nat.PERIODIC, J, -1.0, 1, flags,
             yp, tp)))]
 
-    def runners(self, flags, graph):
-        """[(family, run())]: graph replays (recorded once) or direct calls."""
-        out = []
-        for fam, fn in self.passes(flags):
-            if graph:
-                key = (fam, flags)
-                if key not in self.graphs:
-                    fn()  # first call outside capture: LDS attributes, workspaces, occupancy queries
-                    self.graphs[key] = self.eng.capture(fn)
-                g = self.graphs[key]
-                out.append((fam, lambda g=g: g.launch(1)))
-            else:
-                out.append((fam, fn))
-        return out
+    def step_fn(self, flags):
+        fns = [fn for _, fn in self.passes(flags)]
+
+        def step():
+            for fn in fns:
+                fn()
+        return step
 
     def close(self):
         for g in self.graphs.values():
@@ -217,31 +218,58 @@ class Workload:
         self.graphs.clear()
 
 
-def timed(torch, dist, world, runs, steps, events):
-    """K steps between barrier + synchronize; per-pass HIP events inside the loop. -> (elapsed, {fam: [ms]})."""
-    evs = []
-    if events:
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(len(runs) + 1)] for _ in range(steps)]
+PASS_FAMILIES = {"forward": ("forward", "forward_level"), "inverse": ("inverse", "inverse_level"),
+                 "sigma": ("sigma",)}
+
+
+def measure(torch, dist, world, eng, wl, flags, mode, steps, warmup, settle_s, events):
+    """Settle, warm up, then time exactly `steps` steps between barrier + synchronize.
+
+    mode "graph-k" (default): the K timed steps are recorded once into ONE graph and replayed once --
+    no host work inside the timed region; with `events`, every kernel launch is bracketed by HIP
+    event nodes inside that graph (live per-kernel times of the timed steps).  "graph-step": a
+    one-step graph replayed K times.  "direct": C-ABI calls (events via the engine's launch timer).
+    Returns (elapsed_s, settle (s, steps), {family: (total_ms, launches)}).
+    """
+    step = wl.step_fn(flags)
+    step()  # outside any capture: LDS attributes, workspaces, occupancy queries
+    torch.cuda.synchronize()
+    if mode == "direct":
+        run1 = step
+    else:
+        g1 = eng.capture(step)
+        wl.graphs[("step", flags)] = g1
+        run1 = lambda: g1.launch(1)  # noqa: E731
+    st = settle(torch, run1, settle_s)
+    for _ in range(warmup):
+        run1()
+    torch.cuda.synchronize()
+    eng.reset_timing()
+    if mode == "graph-k":
+        eng.enable_timing(events)
+        gk = eng.capture(lambda: [step() for _ in range(steps)])
+        wl.graphs[("k", flags)] = gk
+        body = lambda: gk.launch(1)  # noqa: E731
+    else:
+        eng.enable_timing(events and mode == "direct")
+        body = lambda: [run1() for _ in range(steps)]  # noqa: E731
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(steps):
-        if events:
-            evs[k][0].record()
-        for i, (_, run) in enumerate(runs):
-            run()
-            if events:
-                evs[k][i + 1].record()
+    body()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    per = {fam: [] for fam, _ in runs}
-    for e in evs:
-        for i, (fam, _) in enumerate(runs):
-            per[fam].append(e[i].elapsed_time(e[i + 1]))
-    return elapsed, per
+    fams = {}
+    for k in ("forward", "inverse", "sigma", "forward_level", "inverse_level"):
+        ms, n = eng.kernel_time(k)
+        if n:
+            fams[k] = (ms, n)
+    eng.enable_timing(False)
+    eng.reset_timing()
+    return elapsed, st, fams
 
 
 def max_over_ranks(torch, dist, world, v, dev):
@@ -252,7 +280,7 @@ def max_over_ranks(torch, dist, world, v, dev):
     return t.item()
 
 
-def settle(torch, runs, seconds):
+def settle(torch, run1, seconds):
     """Replay the step untimed until `seconds` have passed (GPU clock settle); returns (s, steps)."""
     if seconds <= 0:
         return 0.0, 0
@@ -260,30 +288,10 @@ def settle(torch, runs, seconds):
     n = 0
     while time.perf_counter() - t0 < seconds:
         for _ in range(10):
-            for _, run in runs:
-                run()
+            run1()
         n += 10
         torch.cuda.synchronize()
     return time.perf_counter() - t0, n
-
-
-def launch_breakdown(eng, wl, flags, steps):
-    """Kernel launches per pass and per-family HIP-event times from the engine's own launch timer
-    (a short direct-call replay after the timed region; every kernel launch bracketed)."""
-    eng.reset_timing()
-    eng.enable_timing(True)
-    for _ in range(steps):
-        for _, fn in wl.passes(flags):
-            fn()
-    import torch
-    torch.cuda.synchronize()
-    eng.enable_timing(False)
-    out = {}
-    for k in ("forward", "inverse", "sigma", "forward_level", "inverse_level"):
-        ms, n = eng.kernel_time(k)
-        if n:
-            out[k] = {"launches_per_step": n / steps, "ms_per_launch": round(ms / n, 5)}
-    return out
 
 
 def run(args, world, rank, local):
@@ -308,54 +316,48 @@ def run(args, world, rank, local):
     # all work on one dedicated (non-default, capturable) stream; the engine binds to it
     torch.cuda.set_stream(torch.cuda.Stream(device=dev))
     flags = 0 if args.exact else nat.FLAG_FMA
-    graph = not args.no_graph
     events = args.events == "inline"
 
     # ---- strong scaling (headline): rank r owns rows [start, start + rows) of the global batch
     start, rows = shard_rows(Bg, world, rank)
     wl = Workload(eng, w, J, rows, N, dtype, pipeline, start, torch)
-    runs = wl.runners(flags, graph)
-    settle_s, settle_steps = settle(torch, runs, args.settle)
-    for _ in range(args.warmup):
-        for _, run_ in runs:
-            run_()
-    torch.cuda.synchronize()
-    elapsed, per = timed(torch, dist, world, runs, args.steps, events)
+    elapsed, (settle_s, settle_steps), fams = measure(torch, dist, world, eng, wl, flags, args.launch, args.steps,
+                                                      args.warmup, args.settle, events)
     elapsed = max_over_ranks(torch, dist, world, elapsed, dev)
     value = Bg * N * args.steps / elapsed / 1e6
 
     # algorithmic bytes per pass: forward reads x, writes J details + approx;
-    # inverse reads J + 1 rows, writes y; denoise = forward + the d_1 median re-read + inverse
+    # inverse reads J + 1 rows, writes y; the denoise sigma pass re-reads d_1
     units = rows * N
-    pass_bytes = {"forward": (J + 2) * esz * units, "inverse": (J + 2) * esz * units,
-                  "denoise": (2 * (J + 2) + 1) * esz * units}
-    fam_ms = {f: sum(v) / len(v) for f, v in per.items() if v}
-    breakdown = launch_breakdown(eng, wl, flags, min(args.steps, 20))
+    pass_bytes = {"forward": (J + 2) * esz * units, "inverse": (J + 2) * esz * units, "sigma": esz * units}
+    kernels = {k: {"launches_per_step": round(n / args.steps, 3), "ms_per_launch": round(ms / n, 5)}
+               for k, (ms, n) in fams.items()}
+    pass_ms = {}
+    for p_, members in PASS_FAMILIES.items():
+        tot = sum(fams[m][0] for m in members if m in fams)
+        if tot > 0:
+            pass_ms[p_] = tot / args.steps
     roof = None
-    if fam_ms:
-        dom = max(fam_ms, key=lambda f: fam_ms[f])
-        achieved = pass_bytes[dom] / (fam_ms[dom] * 1e-3) / 1e9
+    if pass_ms:
+        dom = max(pass_ms, key=lambda f: pass_ms[f])
+        achieved = pass_bytes[dom] / (pass_ms[dom] * 1e-3) / 1e9
         traffic, tsrc = committed_traffic(args.config, dom)
-        kern = {"forward": "forward pass", "inverse": "inverse pass", "denoise": "denoise step"}[dom]
-        roof = {"bound": "hbm", "kernel": f"{kern} ({launches_desc(breakdown, dom)})", "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic, "traffic_source": tsrc,
-                "algorithmic_bytes_per_launch": pass_bytes[dom], "avg_launch_ms": round(fam_ms[dom], 5)}
+        members = [f"{m} x{kernels[m]['launches_per_step']:g}" for m in PASS_FAMILIES[dom] if m in kernels]
+        roof = {"bound": "hbm", "kernel": f"{dom} pass ({', '.join(members)} launches per step)",
+                "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": tsrc,
+                "algorithmic_bytes_per_launch": pass_bytes[dom], "avg_launch_ms": round(pass_ms[dom], 5)}
 
     # ---- the other accumulation mode, same rows, timed the same way (beside the headline)
     alt = None
     if not args.no_alt:
         aflags = flags ^ nat.FLAG_FMA
-        aruns = wl.runners(aflags, graph)
-        for _ in range(args.warmup):
-            for _, run_ in aruns:
-                run_()
-        torch.cuda.synchronize()
-        ael, aper = timed(torch, dist, world, aruns, args.steps, events)
+        ael, _, afams = measure(torch, dist, world, eng, wl, aflags, args.launch, args.steps, args.warmup, 0.0,
+                                events)
         ael = max_over_ranks(torch, dist, world, ael, dev)
         alt = {"accumulation": ACC_NAME[bool(aflags & nat.FLAG_FMA)],
                "value": round(Bg * N * args.steps / ael / 1e6, 2),
-               "passes_ms": {f: round(sum(v) / len(v), 5) for f, v in aper.items() if v}}
+               "kernels_ms": {k: round(ms / n, 5) for k, (ms, n) in afams.items()}}
     wl.close()
     del wl
 
@@ -363,13 +365,8 @@ def run(args, world, rank, local):
     weak = None
     if world > 1 and not args.no_weak:
         wk = Workload(eng, w, J, Bg, N, dtype, pipeline, rank * Bg, torch)
-        wruns = wk.runners(flags, graph)
-        settle(torch, wruns, min(args.settle, 0.3))
-        for _ in range(args.warmup):
-            for _, run_ in wruns:
-                run_()
-        torch.cuda.synchronize()
-        wel, _ = timed(torch, dist, world, wruns, args.steps, False)
+        wel, _, _ = measure(torch, dist, world, eng, wk, flags, args.launch, args.steps, args.warmup,
+                            min(args.settle, 0.3), False)
         wel = max_over_ranks(torch, dist, world, wel, dev)
         weak = {"value": round(world * Bg * N * args.steps / wel / 1e6, 2), "batch_per_gpu": Bg,
                 "ms_per_step": round(wel / args.steps * 1e3, 4), "global_batch": world * Bg}
@@ -401,11 +398,13 @@ def run(args, world, rank, local):
                 "wavelet": wname, "levels": J, "global_batch": Bg, "batch_per_gpu": rows, "signal_length": N,
                 "boundary": "PERIODIC", "accumulation": ACC_NAME[bool(flags & nat.FLAG_FMA)],
                 "parallelism": f"batch-shard x{world} (contiguous row blocks, no collective)",
-                "launch": "HIP graph per pass (vw_capture_begin / vw_graph_launch)" if graph else "direct C-ABI calls",
-                "passes_ms": {f: round(v, 5) for f, v in fam_ms.items()},
-                "pass_timing": "HIP events on the engine stream around every pass, inside the timed loop"
-                if events else "none",
-                "kernels": breakdown,
+                "launch": LAUNCH_DESC[args.launch],
+                "passes_ms": {f: round(v, 5) for f, v in pass_ms.items()},
+                "kernel_timing": ("HIP events around every kernel launch of the timed steps (event nodes inside "
+                                  "the replayed graph)" if args.launch == "graph-k" else
+                                  "HIP events around every launch (engine timer)" if args.launch == "direct"
+                                  else "none") if events else "none",
+                "kernels": kernels,
                 "other_accumulation": alt,
             },
             "weak_scaling": weak,
@@ -416,13 +415,6 @@ def run(args, world, rank, local):
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
-
-
-def launches_desc(breakdown, fam):
-    keys = [fam, fam + "_level"] if fam != "denoise" else ["forward", "sigma", "inverse", "forward_level",
-                                                           "inverse_level"]
-    parts = [f"{k} x{v['launches_per_step']:g}" for k, v in breakdown.items() if k in keys]
-    return ", ".join(parts) or fam
 
 
 def committed_traffic(config, fam):

@@ -245,7 +245,10 @@ VW_API int64_t vw_stream_history_length(vw_stream *s, int level);
 typedef struct vw_graph vw_graph;
 VW_API vw_status vw_capture_begin(vw_ctx *ctx);
 VW_API vw_status vw_capture_end(vw_ctx *ctx, vw_graph **out);
-/* Replays the recorded calls `count` times, in order, on the context's stream (asynchronous). */
+/* Replays the recorded calls `count` times, in order, on the context's stream (asynchronous).
+ * Timing enabled during the capture (vw_ctx_enable_timing) records every launch's HIP events as
+ * event nodes of the graph; with timing enabled at launch, vw_ctx_kernel_time then reports the
+ * launches of the last replay of the call. */
 VW_API vw_status vw_graph_launch(vw_graph *graph, int64_t count);
 VW_API vw_status vw_graph_destroy(vw_graph *graph);
 

@@ -101,3 +101,39 @@ def test_f32_tensor_into_f64_only_entry_points(engine):
     engine.threshold_inplace(expect, thr, True)
     engine.threshold_inplace(c, thr, True)
     assert torch.equal(c, expect)
+
+
+def test_timing_inside_captured_graph(engine):
+    # launches recorded with timing enabled carry their own event nodes: one replay of a K-step graph
+    # reports K launches per family with positive durations (bench.py's timed region)
+    import torch
+    from ctypes import c_void_p
+    w = Daubechies.DB4
+    B, N, J, K = 32, 4096, 6, 5
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        x, det, app, y = _bufs(torch, B, N, J)
+        engine.fill_uniform(x, 1)
+        lo, hi = nat.taps_array(w.lowPassDecomposition()), nat.taps_array(w.highPassDecomposition())
+        lib, ctx = engine.lib, engine.ctx
+        P = lambda t: c_void_p(t.data_ptr())  # noqa: E731
+
+        def step():
+            assert lib.vw_modwt_forward_f64(ctx, P(x), B, N, N, lo, hi, len(lo), w.wavelet_id, 0, J, nat.FLAG_FMA,
+                                            P(det), P(app)) == 0
+            assert lib.vw_modwt_inverse_f64(ctx, P(det), P(app), B, N, lo, hi, len(lo), w.wavelet_id, 0, J,
+                                            0xFFFFFFFF, 0, nat.FLAG_FMA, P(y)) == 0
+
+        step()
+        engine.reset_timing()
+        engine.enable_timing(True)
+        g = engine.capture(lambda: [step() for _ in range(K)])
+        g.launch(1)
+        torch.cuda.synchronize()
+        for fam in ("forward", "inverse"):
+            ms, n = engine.kernel_time(fam)
+            assert n == K and ms > 0, (fam, ms, n)
+        engine.enable_timing(False)
+        engine.reset_timing()
+        g.close()
+        assert float((y - x).abs().max()) < 1e-9

@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
-"""HBM bytes per launch of each kernel family from rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+"""HBM bytes per PASS (forward / inverse / sigma) from rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
 
 Corrections per /opt/skills/guides/MI355X_MICROARCH.md (HBM / rocprofv3 section): FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of wide (16 B/lane) coalesced
-streaming reads, so it is doubled.  Output: JSON {family: {bytes_per_launch, fetch_bytes, write_bytes,
-dispatches, kernels}} for bench.py's roofline.traffic.
+streaming reads, so it is doubled.  A pass is every kernel launch of one forward (or inverse) call:
+one fused kernel for short signals, a multi-level tile kernel plus column sweeps for long ones.
+Output: JSON {pass: {bytes_per_launch (= per pass), fetch_bytes, write_bytes, dispatches, kernels}}
+plus "captured_at" -- read by bench.py for roofline.traffic.
 
-    python tools/hbm_traffic.py gpurun_out/pmc > profiles/hbm_traffic_db4.json
+    python tools/hbm_traffic.py gpurun_out/pmc_db4 --passes 5 --commit <sha> > profiles/hbm_traffic_db4.json
 """
+import argparse
 import collections
 import csv
 import glob
@@ -15,42 +18,48 @@ import json
 import os
 import sys
 
+MEMBERS = {
+    "forward": ("k_forward_fused", "k_forward_persist", "k_forward_level", "k_forward_multi", "k_forward_sweep"),
+    "inverse": ("k_inverse_fused", "k_inverse_seq", "k_inverse_db", "k_inverse_level", "k_inverse_multi",
+                "k_inverse_sweep"),
+    "sigma": ("k_noise_sigma",),
+}
 
-def family(kernel):
-    k = kernel.split("(")[0].replace("void ", "").replace("vw::", "").strip()
-    if k.startswith("k_forward_fused") or k.startswith("k_forward_persist"):
-        return "forward"
-    if k.startswith("k_inverse_fused") or k.startswith("k_inverse_seq") or k.startswith("k_inverse_db"):
-        return "inverse"
-    if k.startswith("k_forward_level"):
-        return "forward_level"
-    if k.startswith("k_inverse_level"):
-        return "inverse_level"
-    if k.startswith("k_noise_sigma"):
-        return "sigma"
+
+def pass_of(kernel):
+    k = kernel.split("(")[0].replace("void ", "").replace("vw::", "").split("<")[0].strip()
+    for p, names in MEMBERS.items():
+        if k in names:
+            return p
     return None
 
 
 def main():
-    root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+    ap = argparse.ArgumentParser()
+    ap.add_argument("root", nargs="?", default="gpurun_out/pmc")
+    ap.add_argument("--passes", type=int, default=0, help="passes per family in the run (0: one per dispatch)")
+    ap.add_argument("--commit", default="")
+    a = ap.parse_args()
+    # counter -> pass -> list of per-dispatch values (one csv row per dispatch and counter)
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     names = collections.defaultdict(set)
-    for f in sorted(glob.glob(os.path.join(root, "p*", "pmc_counter_collection.csv"))):
+    for f in sorted(glob.glob(os.path.join(a.root, "p*", "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
-            fam = family(r["Kernel_Name"])
-            if fam is None:
+            p = pass_of(r["Kernel_Name"])
+            if p is None:
                 continue
-            vals[fam][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            names[fam].add(r["Kernel_Name"].split("(")[0])
-    out = {}
-    for fam, cs in vals.items():
+            vals[p][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            names[p].add(r["Kernel_Name"].split("(")[0].replace("void ", ""))
+    out = {"captured_at": a.commit or None}
+    for p, cs in vals.items():
         if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
-        fetch = 2.0 * 1024.0 * sum(cs["FETCH_SIZE"]) / len(cs["FETCH_SIZE"])
-        write = 1024.0 * sum(cs["WRITE_SIZE"]) / len(cs["WRITE_SIZE"])
-        out[fam] = {"bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch), "write_bytes": round(write),
-                    "dispatches": len(cs["FETCH_SIZE"]), "kernels": sorted(names[fam]),
-                    "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), KiB -> bytes"}
+        n = a.passes or len(cs["FETCH_SIZE"])
+        fetch = 2.0 * 1024.0 * sum(cs["FETCH_SIZE"]) / n
+        write = 1024.0 * sum(cs["WRITE_SIZE"]) / n
+        out[p] = {"bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch), "write_bytes": round(write),
+                  "dispatches": len(cs["FETCH_SIZE"]), "passes": n, "kernels": sorted(names[p]),
+                  "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), KiB -> bytes; per pass"}
     json.dump(out, sys.stdout, indent=1)
     print()
 

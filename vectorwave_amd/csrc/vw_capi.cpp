@@ -56,6 +56,7 @@ static vw_status ok() {
 struct TimedLaunch {
   std::string family;
   hipEvent_t start, stop;
+  bool graph_owned = false;  // recorded inside a captured graph: its events live as long as the graph
 };
 
 // Tuning switches (A/B experiments, tools/ab_*.sh), read from the environment ONCE per context at
@@ -114,6 +115,7 @@ struct vw_ctx {
   unsigned long long* bad = nullptr;   // device word for the fused non-finite check
   bool timing = false;
   std::vector<TimedLaunch> pending;
+  std::vector<TimedLaunch> captured;   // timed launches recorded during the current capture
   std::vector<hipEvent_t> event_pool;
   std::map<std::string, std::pair<double, int64_t>> totals;
 };
@@ -141,14 +143,50 @@ static hipEvent_t pool_event(vw_ctx* c) {
   return e;
 }
 
-// Brackets a kernel launch with HIP events on the context stream when timing is enabled.
+// An event-record node appended to the graph being captured on `st` (after the current capture
+// dependencies, which it then replaces): the graph-API form of recording a timing event inside a
+// captured sequence.  Falls back to hipEventRecordWithFlags(..., hipEventRecordExternal).  A failed
+// attempt's error is cleared so it does not surface at the next launch's hipGetLastError.
+static bool capture_event(hipStream_t st, hipEvent_t ev) {
+  hipStreamCaptureStatus status;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t ndeps = 0;
+  if (hipStreamGetCaptureInfo_v2(st, &status, &id, &g, &deps, &ndeps) == hipSuccess &&
+      status == hipStreamCaptureStatusActive && g) {
+    hipGraphNode_t node = nullptr;
+    if (hipGraphAddEventRecordNode(&node, g, deps, ndeps, ev) == hipSuccess &&
+        hipStreamUpdateCaptureDependencies(st, &node, 1, hipStreamSetCaptureDependencies) == hipSuccess)
+      return true;
+  }
+  (void)hipGetLastError();
+  if (hipEventRecordWithFlags(ev, st, hipEventRecordExternal) == hipSuccess) return true;
+  (void)hipGetLastError();
+  return false;
+}
+
+// Brackets a kernel launch with HIP events on the context stream when timing is enabled.  While
+// capturing, the events become event-record nodes of the graph (hipEventRecordExternal), owned by
+// the graph: every replay re-records them, so the launch is timed inside the replayed graph.
 struct LaunchTimer {
   vw_ctx* c;
   TimedLaunch tl;
   bool on;
-  LaunchTimer(vw_ctx* ctx, const char* family) : c(ctx), on(ctx->timing && !ctx->capturing) {
+  LaunchTimer(vw_ctx* ctx, const char* family) : c(ctx), on(ctx->timing) {
     if (!on) return;
     tl.family = family;
+    if (c->capturing) {
+      tl.graph_owned = true;
+      tl.start = tl.stop = nullptr;
+      if (hipEventCreate(&tl.start) != hipSuccess || hipEventCreate(&tl.stop) != hipSuccess ||
+          !capture_event(c->stream, tl.start)) {
+        if (tl.start) hipEventDestroy(tl.start);
+        if (tl.stop) hipEventDestroy(tl.stop);
+        on = false;
+      }
+      return;
+    }
     tl.start = pool_event(c);
     tl.stop = pool_event(c);
     if (!tl.start || !tl.stop) { on = false; return; }
@@ -156,6 +194,15 @@ struct LaunchTimer {
   }
   ~LaunchTimer() {
     if (!on) return;
+    if (tl.graph_owned) {
+      if (capture_event(c->stream, tl.stop)) {
+        c->captured.push_back(tl);
+      } else {
+        hipEventDestroy(tl.start);
+        hipEventDestroy(tl.stop);
+      }
+      return;
+    }
     hipEventRecord(tl.stop, c->stream);
     c->pending.push_back(tl);
   }
@@ -169,8 +216,10 @@ static void collect_timing(vw_ctx* c) {
       t.first += ms;
       t.second += 1;
     }
-    c->event_pool.push_back(tl.start);
-    c->event_pool.push_back(tl.stop);
+    if (!tl.graph_owned) {
+      c->event_pool.push_back(tl.start);
+      c->event_pool.push_back(tl.stop);
+    }
   }
   c->pending.clear();
 }
@@ -380,6 +429,7 @@ extern "C" vw_status vw_ctx_set_stream(vw_ctx* c, void* s) {
 struct vw_graph {
   vw_ctx* ctx = nullptr;
   unsigned ws_gen = 0;
+  std::vector<TimedLaunch> timed;  // event-record nodes (timing enabled at capture)
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
 };
@@ -392,6 +442,7 @@ extern "C" vw_status vw_capture_begin(vw_ctx* c) {
   hipSetDevice(c->device);
   VW_HIP(hipStreamBeginCapture(c->stream, hipStreamCaptureModeThreadLocal));
   c->capturing = true;
+  c->captured.clear();
   return ok();
 }
 
@@ -401,15 +452,24 @@ extern "C" vw_status vw_capture_end(vw_ctx* c, vw_graph** out) {
   if (!c->capturing) return fail(VW_ERR_STATE, "not capturing");
   hipSetDevice(c->device);
   c->capturing = false;
+  std::vector<TimedLaunch> timed;
+  timed.swap(c->captured);
+  auto drop = [&] { for (auto& t : timed) { hipEventDestroy(t.start); hipEventDestroy(t.stop); } };
   hipGraph_t graph = nullptr;
-  VW_HIP(hipStreamEndCapture(c->stream, &graph));
+  hipError_t ec = hipStreamEndCapture(c->stream, &graph);
+  if (ec != hipSuccess) {
+    drop();
+    return fail(VW_ERR_DEVICE, "hipStreamEndCapture: %s", hipGetErrorString(ec));
+  }
   hipGraphExec_t exec = nullptr;
   hipError_t e = hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0);
   if (e != hipSuccess) {
     hipGraphDestroy(graph);
+    drop();
     return fail(VW_ERR_DEVICE, "graph instantiate failed: %s", hipGetErrorString(e));
   }
   vw_graph* gr = new vw_graph();
+  gr->timed.swap(timed);
   gr->ctx = c;
   gr->ws_gen = c->ws_gen;
   gr->graph = graph;
@@ -426,13 +486,20 @@ extern "C" vw_status vw_graph_launch(vw_graph* gr, int64_t count) {
     return fail(VW_ERR_STATE, "the context workspace moved since this graph was recorded; record it again");
   hipSetDevice(c->device);
   for (int64_t i = 0; i < count; ++i) VW_HIP(hipGraphLaunch(gr->exec, c->stream));
+  // timed launches recorded inside the graph: their events hold the LAST replay of this call
+  if (c->timing && count > 0)
+    for (const auto& t : gr->timed) c->pending.push_back(t);
   return ok();
 }
 
 extern "C" vw_status vw_graph_destroy(vw_graph* gr) {
   if (!gr) return fail(VW_ERR_NULL, "graph is null");
-  hipSetDevice(gr->ctx->device);
-  hipStreamSynchronize(gr->ctx->stream);
+  vw_ctx* c = gr->ctx;
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  hipStreamSynchronize(c->stream);
+  collect_timing(c);  // pending entries may reference this graph's events
+  for (auto& t : gr->timed) { hipEventDestroy(t.start); hipEventDestroy(t.stop); }
   if (gr->exec) hipGraphExecDestroy(gr->exec);
   if (gr->graph) hipGraphDestroy(gr->graph);
   delete gr;
