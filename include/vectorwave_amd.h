@@ -131,6 +131,10 @@ VW_API vw_status vw_ctx_set_stream(vw_ctx *ctx, void *hip_stream);
 /* Enqueue on the device's null (legacy default) stream, e.g. torch's default stream (handle 0). */
 VW_API vw_status vw_ctx_use_null_stream(vw_ctx *ctx);
 VW_API void *vw_ctx_get_stream(vw_ctx *ctx);
+/* Kernel-path switches of this context (A/B experiments, tests), named like the environment
+ * variables read once at vw_ctx_create (VW_FORCE_TILED, VW_MULTI_TILE, VW_INV_BLK, VW_NV, ...);
+ * value < 0 restores the default.  VW_ERR_ARG for an unknown name. */
+VW_API vw_status vw_ctx_set_option(vw_ctx *ctx, const char *key, int value);
 VW_API vw_status vw_ctx_synchronize(vw_ctx *ctx);
 VW_API int vw_ctx_device(vw_ctx *ctx);
 

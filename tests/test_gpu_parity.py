@@ -305,21 +305,18 @@ def test_forward_persistent_matches_per_signal_kernel(engine, case):
     dtype = torch.float64 if dt == "f64" else torch.float32
     x = torch.empty((B, n), dtype=dtype, device="cuda")
     engine.fill_uniform(x, 5)
-    old = {k: os.environ.get(k) for k in ("VW_FWD_PERSIST", "VW_FWD_BUF")}
-    try:
-        if buf:
-            os.environ["VW_FWD_BUF"] = buf
-        outs = []
-        for persist in ("0", "1"):
-            os.environ["VW_FWD_PERSIST"] = persist
-            outs.append(engine.forward(x, *lohi(w), w.wavelet_id, boundary, J, flags))
+    outs = []
+    for nv in (4, 8):
+        for persist in (0, 1):
+            opts = dict(VW_FWD_PERSIST=persist, VW_NV=nv)
+            if buf:
+                opts["VW_FWD_BUF"] = int(buf)
+            with engine.options(**opts):
+                outs.append(engine.forward(x, *lohi(w), w.wavelet_id, boundary, J, flags))
             torch.cuda.synchronize()
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    for d_, a_ in outs[2:]:  # the NV = 8 kernels (half the threads) compute the same bits
+        assert torch.equal(d_, outs[0][0]) and torch.equal(a_, outs[0][1])
+    outs = outs[:2]
     (d0, a0), (d1, a1) = outs
     assert torch.equal(d0, d1) and torch.equal(a0, a1)
     xh = x.double().cpu().numpy()
@@ -354,50 +351,75 @@ def test_fp32_path(engine):
 
 
 # ---- tiled (long-signal) path ---------------------------------------------------------------------------
-def test_tiled_path_bit_exact(engine, monkeypatch):
-    monkeypatch.setenv("VW_FORCE_TILED", "1")
+def test_tiled_path_bit_exact(engine):
     # levels with spacing >= 16 run as column sweeps (N % s != 0 exercises wraps across residues)
-    for w, boundary, n, J in [(Daubechies.DB4, O.PERIODIC, 10000, 6), (Daubechies.DB8, O.SYMMETRIC, 5000, 4),
-                              (Symlet.SYM8, O.ZERO_PADDING, 9000, 5), (Daubechies.DB8, O.SYMMETRIC, 7001, 6),
-                              (Coiflet.COIF5, O.PERIODIC, 20000, 6),
-                              (Daubechies.DB4, O.SYMMETRIC, 4099, 8)]:
-        x = signals(2, n, 19)
-        tx = vw.MultiLevelMODWTTransform(w, vw.BoundaryMode(boundary))
-        res = tx.decompose(x, J)
-        y = tx.reconstruct(res)
-        for b in range(2):
-            d, a = O.decompose(x[b], *lohi(w), boundary, J)
-            exact(res.details_array[:, b, :], d)
-            exact(res.approximation_array[b], a)
-            exact(y[b], O.reconstruct(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), boundary,
-                                      w.wavelet_id))
+    with engine.options(VW_FORCE_TILED=1):
+        for w, boundary, n, J in [(Daubechies.DB4, O.PERIODIC, 10000, 6), (Daubechies.DB8, O.SYMMETRIC, 5000, 4),
+                                  (Symlet.SYM8, O.ZERO_PADDING, 9000, 5), (Daubechies.DB8, O.SYMMETRIC, 7001, 6),
+                                  (Coiflet.COIF5, O.PERIODIC, 20000, 6),
+                                  (Daubechies.DB4, O.SYMMETRIC, 4099, 8)]:
+            x = signals(2, n, 19)
+            tx = vw.MultiLevelMODWTTransform(w, vw.BoundaryMode(boundary))
+            res = tx.decompose(x, J)
+            y = tx.reconstruct(res)
+            for b in range(2):
+                d, a = O.decompose(x[b], *lohi(w), boundary, J)
+                exact(res.details_array[:, b, :], d)
+                exact(res.approximation_array[b], a)
+                exact(y[b], O.reconstruct(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), boundary,
+                                          w.wavelet_id))
 
 
-@pytest.mark.parametrize("tile", ["128", "2048"])
-def test_multilevel_tiles_bit_exact(engine, monkeypatch, tile):
+@pytest.mark.parametrize("tile", [128, 2048])
+def test_multilevel_tiles_bit_exact(engine, tile):
     # long PERIODIC signals run groups of levels per tile (vw_capi.cpp level_groups): odd N (scalar
     # I/O), N not a multiple of the tile, tiles shorter than the reach (wraps through the halo), and
     # the SWT denoise thresholds applied on the detail loads; EXACT mode is bit-exact
-    monkeypatch.setenv("VW_FORCE_TILED", "1")
-    monkeypatch.setenv("VW_MULTI_TILE", tile)
-    for w, n, J in [(Daubechies.DB4, 10000, 6), (Daubechies.DB8, 30001, 8), (H, 5000, 9),
-                    (Coiflet.COIF5, 20000, 5), (Symlet.SYM8, 4097, 6)]:   # J=7 would enter the FFT region
-        x = signals(2, n, 23)
-        tx = vw.MultiLevelMODWTTransform(w, vw.BoundaryMode.PERIODIC)
-        res = tx.decompose(x, J)
-        y = tx.reconstruct(res)
+    with engine.options(VW_FORCE_TILED=1, VW_MULTI_TILE=tile):
+        for w, n, J in [(Daubechies.DB4, 10000, 6), (Daubechies.DB8, 30001, 8), (H, 5000, 9),
+                        (Coiflet.COIF5, 20000, 5), (Symlet.SYM8, 4097, 6)]:   # J=7 would enter the FFT region
+            x = signals(2, n, 23)
+            tx = vw.MultiLevelMODWTTransform(w, vw.BoundaryMode.PERIODIC)
+            res = tx.decompose(x, J)
+            y = tx.reconstruct(res)
+            for b in range(2):
+                d, a = O.decompose(x[b], *lohi(w), O.PERIODIC, J)
+                exact(res.details_array[:, b, :], d)
+                exact(res.approximation_array[b], a)
+                exact(y[b], O.reconstruct(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC))
+        w, n, J = Symlet.SYM8, 12000, 5
+        x = signals(2, n, 29)
+        y, thr = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC).denoise(x, J, return_thresholds=True)
         for b in range(2):
-            d, a = O.decompose(x[b], *lohi(w), O.PERIODIC, J)
-            exact(res.details_array[:, b, :], d)
-            exact(res.approximation_array[b], a)
-            exact(y[b], O.reconstruct(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC))
-    w, n, J = Symlet.SYM8, 12000, 5
-    x = signals(2, n, 29)
-    y, thr = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC).denoise(x, J, return_thresholds=True)
-    for b in range(2):
-        y_ref, t_ref = O.swt_denoise(x[b], *lohi(w), O.PERIODIC, J, wavelet_id=w.wavelet_id)
-        assert thr[b] == t_ref
-        exact(y[b], y_ref)
+            y_ref, t_ref = O.swt_denoise(x[b], *lohi(w), O.PERIODIC, J, wavelet_id=w.wavelet_id)
+            assert thr[b] == t_ref
+            exact(y[b], y_ref)
+
+
+# ---- alternative fused inverse kernels (selected by policy or option) ------------------------------------
+@pytest.mark.parametrize("opts", [dict(VW_INV_BUF=2), dict(VW_NV=8), dict(VW_INV_BUF=2, VW_NV=8)],
+                         ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
+@pytest.mark.parametrize("fma", [False, True], ids=["exact", "fma"])
+def test_inverse_kernel_variants_bit_exact(engine, opts, fma):
+    # every variant computes the reference's sums in the reference's order: EXACT bit-exact, FMA equal
+    # to the default FMA kernel (same per-output operation sequence)
+    cases = [(Daubechies.DB4, 4096, 6, 8), (Daubechies.DB4, 4096, 9, 3), (Symlet.SYM8, 4096, 8, 3),
+             (H, 2048, 7, 4), (Daubechies.DB8, 1024, 5, 5), (Coiflet.COIF5, 8192, 6, 2)]
+    for w, n, J, B in cases:
+        x = signals(B, n, 41)
+        tx = vw.MultiLevelMODWTTransform(w, vw.BoundaryMode.PERIODIC, fma=fma)
+        res = tx.decompose(x, J)
+        y0 = tx.reconstruct(res)
+        with engine.options(**opts):
+            y1 = tx.reconstruct(res)
+            y2 = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC, fma=fma).denoise(x, J)
+        y2_ref = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC, fma=fma).denoise(x, J)
+        exact(y1, y0)
+        exact(y2, y2_ref)
+        if not fma:
+            for b in range(B):
+                d, a = res.details_array[:, b, :], res.approximation_array[b]
+                exact(y1[b], O.reconstruct(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC))
 
 
 def test_long_block_db8_j10(engine):

@@ -34,6 +34,7 @@ SIGNATURES = {
     "vw_ctx_use_null_stream": (c_int, [c_void_p]),
     "vw_ctx_set_stream": (c_int, [c_void_p, c_void_p]),
     "vw_ctx_get_stream": (c_void_p, [c_void_p]),
+    "vw_ctx_set_option": (c_int, [c_void_p, c_char_p, c_int]),
     "vw_ctx_synchronize": (c_int, [c_void_p]),
     "vw_ctx_device": (c_int, [c_void_p]),
     "vw_last_error": (c_char_p, []),

@@ -78,25 +78,43 @@ struct Tuning {
   int sweep_qc = kSweepChunk;  // VW_SWEEP_QC: q-chunk per sweep thread
 };
 
+// One switch of the Tuning struct by its environment name; value < 0 = the default.  Returns false
+// for an unknown name.
+static bool set_tuning(Tuning& t, const char* key, int v) {
+  const Tuning d;
+  const std::string k(key);
+  if (k == "VW_NV") t.nv = v < 0 ? d.nv : v <= 4 ? 4 : 8;
+  else if (k == "VW_FWD_PERSIST") t.fwd_persist = v < 0 ? d.fwd_persist : v != 0;
+  else if (k == "VW_FWD_BUF") t.fwd_buf = v < 0 ? d.fwd_buf : v;
+  else if (k == "VW_FORCE_TILED") t.force_tiled = v > 0;
+  else if (k == "VW_FWD_REV") t.fwd_rev = v < 0 ? 0 : v;
+  else if (k == "VW_INV_REV") t.inv_rev = v < 0 ? 0 : v;
+  else if (k == "VW_FWD_TILE") t.fwd_tile = v < 0 ? 0 : v;
+  else if (k == "VW_MULTI") t.multi = v < 0 ? d.multi : v != 0;
+  else if (k == "VW_MULTI_DIV") t.multi_div = v <= 0 ? d.multi_div : v;
+  else if (k == "VW_MULTI_TILE") t.multi_tile = v < 0 ? 0 : v;
+  else if (k == "VW_INV_BUF") t.inv_buf = v < 0 ? 0 : v;
+  else if (k == "VW_INV_TILE") t.inv_tile = v < 0 ? 0 : v;
+  else if (k == "VW_MULTI_RBLK") t.multi_rblk = v < 0 ? d.multi_rblk : v;
+  else if (k == "VW_NO_SWEEP") t.no_sweep = v > 0;
+  else if (k == "VW_SWEEP_QC") t.sweep_qc = v >= 16 ? v : d.sweep_qc;
+  else return false;
+  return true;
+}
+
+static const char* const kTuningKeys[] = {
+    "VW_NV", "VW_FWD_PERSIST", "VW_FWD_BUF", "VW_FORCE_TILED", "VW_FWD_REV", "VW_INV_REV",
+    "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_NO_SWEEP", "VW_SWEEP_QC"};
+
 static Tuning read_tuning() {
   Tuning t;
-  auto iv = [](const char* k, int def) { const char* e = getenv(k); return e ? atoi(e) : def; };
-  t.nv = iv("VW_NV", 4) <= 4 ? 4 : 8;
-  t.fwd_persist = iv("VW_FWD_PERSIST", 1) != 0;
-  t.fwd_buf = iv("VW_FWD_BUF", 0);
-  t.force_tiled = getenv("VW_FORCE_TILED") != nullptr;
-  t.fwd_rev = iv("VW_FWD_REV", 0);
-  t.inv_rev = iv("VW_INV_REV", 0);
-  t.fwd_tile = iv("VW_FWD_TILE", 0);
-  t.multi = iv("VW_MULTI", 1) != 0;
-  t.multi_div = std::max(1, iv("VW_MULTI_DIV", 4));
-  t.multi_tile = iv("VW_MULTI_TILE", 0);
-  t.inv_buf = iv("VW_INV_BUF", 0);
-  t.inv_tile = iv("VW_INV_TILE", 0);
-  t.multi_rblk = iv("VW_MULTI_RBLK", 1);
-  t.no_sweep = getenv("VW_NO_SWEEP") != nullptr;
-  const int qc = iv("VW_SWEEP_QC", kSweepChunk);
-  t.sweep_qc = qc >= 16 ? qc : kSweepChunk;
+  for (const char* k : kTuningKeys) {
+    const char* e = getenv(k);
+    if (!e) continue;
+    // presence-style switches (VW_FORCE_TILED, VW_NO_SWEEP) are on when set to anything but "0"
+    const int v = (*e == '\0') ? 1 : atoi(e);
+    set_tuning(t, k, v);
+  }
   return t;
 }
 
@@ -506,6 +524,13 @@ extern "C" vw_status vw_graph_destroy(vw_graph* gr) {
   return ok();
 }
 
+extern "C" vw_status vw_ctx_set_option(vw_ctx* c, const char* key, int value) {
+  if (!c || !key) return fail(VW_ERR_NULL, "null argument");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (!set_tuning(c->tune, key, value)) return fail(VW_ERR_ARG, "unknown option %s", key);
+  return ok();
+}
+
 extern "C" void* vw_ctx_get_stream(vw_ctx* c) { return c ? (void*)c->stream : nullptr; }
 extern "C" int vw_ctx_device(vw_ctx* c) { return c ? c->device : -1; }
 
@@ -775,7 +800,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     const bool persist = dbl && a.unrolled && persist_ok(threads, nv, fit);
     {
       LaunchTimer lt(c, "forward");
-      hipError_t e = persist ? launch_forward_persist<T>(a, threads, lds, fma, c->stream)
+      hipError_t e = persist ? launch_forward_persist<T>(a, threads, lds, fma, nv, c->stream)
                              : launch_forward_fused<T>(a, threads, lds, fma, nv, c->stream);
       if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward launch failed: %s", hipGetErrorString(e));
     }
@@ -943,11 +968,6 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     memset(&a, 0, sizeof(a));
     a.details = details; a.approx = approx; a.y = y; a.B = B; a.N = (int)N; a.J = J;
     a.db = db ? 1 : 0;
-    a.hlpad_a = hlpad; a.hlpad_d = hlpad; a.region_d = (int)region;
-    a.vec_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
-    a.unrolled = a.vec_io && fit;
-    a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.thr_ld = thr_ld; a.soft = soft; a.taps = L;
-    a.rev = tu.inv_rev;
     copy_taps(a.lo, lo, L);
     copy_taps(a.hi, hi, L);
     for (int j = 0; j < J; ++j) a.lv[j] = lv[j];

@@ -46,6 +46,16 @@ __device__ __forceinline__ T madd(T acc, T x, T f) {
   else return acc + x * f;
 }
 
+// Workgroup-uniform read of data written before the launch (thresholds, per-signal constants)
+// through the constant address space: a scalar (SMEM) load.  A vector load of it inside a level loop
+// would make the waitcnt pass, which cannot count across the loop's conditional load, wait vmcnt(0)
+// at the loop head -- i.e. for the detail-row prefetch that is meant to stay in flight.
+template <typename T>
+__device__ __forceinline__ T load_uniform(const T* q) {
+  typedef const __attribute__((address_space(4))) T* cptr;
+  return *(cptr)(q);
+}
+
 __device__ __forceinline__ bool finite_t(double v) { return __builtin_isfinite(v); }
 __device__ __forceinline__ bool finite_t(float v) { return __builtin_isfinite(v); }
 
@@ -661,7 +671,10 @@ __device__ __forceinline__ void fwd_level(const FwdArgs<T>& p, const T* X, int n
   });
 }
 
-template <typename T, int L, bool FMA, int NV>
+// HIST: streaming history halos (kHaloHistory) possible.  The history is the only global load inside
+// the level loop; without it (HIST = false) no load can be pending there, so the waitcnt pass never
+// waits vmcnt(0) -- which on gfx950 would also wait for every detail store still in flight.
+template <typename T, int L, bool FMA, int NV, bool HIST>
 __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_fused(const FwdArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -676,6 +689,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_fused(const FwdA
   const bool vec_ok = (L > 0) || p.vec_io != 0;  // unrolled kernels run with aligned rows only
   const unsigned long long flat0 = (unsigned long long)b * (unsigned long long)N;
   auto hist_of = [&](int j) -> const T* {  // level j's streaming history row (or nullptr)
+    if constexpr (!HIST) return nullptr;
     const LevelDesc& d = p.lv[j - 1];
     return d.mode == kHaloHistory ? p.hist[j - 1] + b * d.hist_len : nullptr;
   };
@@ -701,7 +715,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_fused(const FwdA
     else fwd_level<T, L, FMA, NV, false>(p, X, nvec, lv, dout, aout, vec_ok, flat0, areg);
     // Streaming: new left history = last hist_len samples of this level's input
     // (BatchStreamingMODWT.updateHistoryFromSoA :337-352).
-    if (p.hist_update && lv.hist_len > 0) {
+    if (HIST && p.hist_update && lv.hist_len > 0) {
       T* hnew = p.hist[j - 1] + b * lv.hist_len;
       for (int q = tid; q < lv.hist_len; q += NT) hnew[q] = X[q + N - lv.hist_len];
     }
@@ -813,7 +827,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_fused(const InvA
   const int nvec = (N + V - 1) / V;
   const bool vec_ok = (L > 0) || p.vec_io != 0;
   // threshold of level j (denoise): thr[(j-1)*thr_ld + b]; thr_ld = 0 -> one threshold for every level
-  auto thr_of = [&](int j) { return p.thr ? p.thr[(size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b] : T(0); };
+  auto thr_of = [&](int j) { return p.thr ? load_uniform(p.thr + (size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b) : T(0); };
   const size_t plane = (size_t)p.B * (size_t)N;
 
   T reg[NV][V];
@@ -873,7 +887,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_db(const InvArgs
   const int nvec = (N + V - 1) / V;
   const bool vec_ok = (L > 0) || p.vec_io != 0;
   // threshold of level j (denoise): thr[(j-1)*thr_ld + b]; thr_ld = 0 -> one threshold for every level
-  auto thr_of = [&](int j) { return p.thr ? p.thr[(size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b] : T(0); };
+  auto thr_of = [&](int j) { return p.thr ? load_uniform(p.thr + (size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b) : T(0); };
   const size_t plane = (size_t)p.B * (size_t)N;
 
   T acc[NV][V];
@@ -913,7 +927,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_seq(const InvArg
   const int nvec = (N + V - 1) / V;
   const bool vec_ok = (L > 0) || p.vec_io != 0;
   // threshold of level j (denoise): thr[(j-1)*thr_ld + b]; thr_ld = 0 -> one threshold for every level
-  auto thr_of = [&](int j) { return p.thr ? p.thr[(size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b] : T(0); };
+  auto thr_of = [&](int j) { return p.thr ? load_uniform(p.thr + (size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b) : T(0); };
   const size_t plane = (size_t)p.B * (size_t)N;
 
   T acc[NV][V];

@@ -6,9 +6,10 @@ namespace vw {
 
 template <typename T, int L, bool FMA, int NV>
 static hipError_t run_forward_fused_nv(const FwdArgs<T>& a, int threads, int lds, hipStream_t st) {
-  auto k = k_forward_fused<T, L, FMA, NV>;
-  static int configured = 64 * 1024;
-  hipError_t e = set_lds(k, lds, &configured);
+  const bool hist = a.hist[0] != nullptr;
+  auto k = hist ? k_forward_fused<T, L, FMA, NV, true> : k_forward_fused<T, L, FMA, NV, false>;
+  static int configured = 64 * 1024, configured_h = 64 * 1024;
+  hipError_t e = set_lds(k, lds, hist ? &configured_h : &configured);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(threads), lds, st, a);
   return hipGetLastError();
@@ -33,9 +34,9 @@ hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds, bool 
 template hipError_t launch_forward_fused<VW_T>(const FwdArgs<VW_T>&, int, int, bool, int, hipStream_t);
 // Persistent forward (k_forward_persist): as many workgroups as are resident at once, each walking
 // signals blockIdx.x + k*gridDim.x.  The resident count comes from the occupancy API (LDS-bound).
-template <typename T, int L, bool FMA>
+template <typename T, int L, bool FMA, int NV>
 static hipError_t run_forward_persist(const FwdArgs<T>& a, int threads, int lds, hipStream_t st) {
-  auto k = k_forward_persist<T, L, FMA, 4>;
+  auto k = k_forward_persist<T, L, FMA, NV>;
   static int configured = 64 * 1024;
   hipError_t e = set_lds(k, lds, &configured);
   if (e != hipSuccess) return e;
@@ -59,16 +60,22 @@ static hipError_t run_forward_persist(const FwdArgs<T>& a, int threads, int lds,
   return hipGetLastError();
 }
 
+template <typename T, int L, bool FMA>
+static hipError_t run_forward_persist_nv(const FwdArgs<T>& a, int threads, int lds, int nv, hipStream_t st) {
+  (void)nv;  // NV = 4 only (host contract)
+  return run_forward_persist<T, L, FMA, 4>(a, threads, lds, st);
+}
+
 template <typename T>
-hipError_t launch_forward_persist(const FwdArgs<T>& a, int threads, int lds, bool fma, hipStream_t st) {
+hipError_t launch_forward_persist(const FwdArgs<T>& a, int threads, int lds, bool fma, int nv, hipStream_t st) {
   switch (a.taps) {
 #define VW_CASE(n) \
-    case n: return fma ? run_forward_persist<T, n, true>(a, threads, lds, st) : run_forward_persist<T, n, false>(a, threads, lds, st);
+    case n: return fma ? run_forward_persist_nv<T, n, true>(a, threads, lds, nv, st) : run_forward_persist_nv<T, n, false>(a, threads, lds, nv, st);
     VW_TAP_LIST(VW_CASE)
 #undef VW_CASE
     default:
       return hipErrorNotSupported;
   }
 }
-template hipError_t launch_forward_persist<VW_T>(const FwdArgs<VW_T>&, int, int, bool, hipStream_t);
+template hipError_t launch_forward_persist<VW_T>(const FwdArgs<VW_T>&, int, int, bool, int, hipStream_t);
 }  // namespace vw

@@ -164,7 +164,7 @@ struct DenoiseConsts {
 template <typename T>
 hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
 template <typename T>
-hipError_t launch_forward_persist(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, hipStream_t st);
+hipError_t launch_forward_persist(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
 template <typename T>
 hipError_t launch_inverse_fused(const InvArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
 template <typename T>

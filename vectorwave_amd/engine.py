@@ -69,6 +69,25 @@ class Engine:
                    self.lib.vw_ctx_set_stream(self.ctx, c_void_p(s)))
             self._ext_stream = s
 
+    def set_option(self, key: str, value: int) -> None:
+        """Kernel-path switch of this context (vw_ctx_set_option); value < 0 = default."""
+        _check(self.lib.vw_ctx_set_option(self.ctx, key.encode(), int(value)))
+
+    def options(self, **kv):
+        """Context manager: set switches (VW_... = int) for the block, restore the defaults after."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def cm():
+            for k, v in kv.items():
+                self.set_option(k, v)
+            try:
+                yield self
+            finally:
+                for k in kv:
+                    self.set_option(k, -1)
+        return cm()
+
     def synchronize(self) -> None:
         _check(self.lib.vw_ctx_synchronize(self.ctx))
 
