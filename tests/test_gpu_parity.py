@@ -591,3 +591,44 @@ def test_forward_strided_rows_ldx(engine):
                                 flags)
         torch.cuda.synchronize()
         assert torch.equal(det, d2) and torch.equal(app, a2)
+
+
+# ---- register-blocked PERIODIC kernels (long filters, vw_device.h k_forward_blk / k_inverse_blk) --------
+@pytest.mark.parametrize("case", [("sym8", 16384, 8, "f64", 3), ("sym8", 4096, 8, "f64", 5), ("db8", 4096, 6, "f64", 5),
+                                  ("coif5", 8192, 6, "f32", 6), ("coif5", 4096, 5, "f64", 3), ("db6", 2048, 7, "f64", 4)],
+                         ids=lambda c: f"{c[0]}-{c[1]}-J{c[2]}-{c[3]}")
+@pytest.mark.parametrize("fma", [False, True], ids=["exact", "fma"])
+def test_blocked_kernels_match_default(engine, case, fma):
+    # the blocked kernels run every output's taps in the same order as the one-vector-per-tap kernels:
+    # identical bits (EXACT and FMA), and EXACT equals the restatement
+    import torch
+    wname, n, J, dt, B = case
+    w = vw.get_wavelet(wname)
+    dtype = torch.float64 if dt == "f64" else torch.float32
+    x = torch.from_numpy(O.fill_uniform(B * n, 9).reshape(B, n)).to(dtype).cuda()
+    flags = nat.FLAG_FMA if fma else 0
+    out = {}
+    for blk in (0, 2):
+        with engine.options(VW_BLK=blk):
+            d, a = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, J, flags)
+            y = engine.inverse(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), w.wavelet_id, O.PERIODIC,
+                               J, flags)
+            torch.cuda.synchronize()
+            out[blk] = (d, a, y)
+    for t0, t1 in zip(out[0], out[2]):
+        assert torch.equal(t0, t1)
+    if dt == "f64" and not fma:
+        d, a, y = (t.cpu().numpy() for t in out[2])
+        xh = x.cpu().numpy()
+        for b in (0, B - 1):
+            d_ref, a_ref = O.decompose(xh[b], *lohi(w), O.PERIODIC, J, core=False)
+            exact(d[:, b, :], d_ref)
+            exact(a[b], a_ref)
+            exact(y[b], O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC))
+    if wname == "sym8" and n == 16384 and not fma:
+        # the config-3 denoise through the blocked kernels: thresholds and outputs bit-exact
+        y2, thr = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC).denoise(x.cpu().numpy(), J, return_thresholds=True)
+        for b in (0, B - 1):
+            y_ref, t_ref = O.swt_denoise(x[b].cpu().numpy(), *lohi(w), O.PERIODIC, J, wavelet_id=w.wavelet_id)
+            assert thr[b] == t_ref
+            exact(y2[b], y_ref)

@@ -76,6 +76,8 @@ struct Tuning {
   int multi_rblk = 1;      // VW_MULTI_RBLK: register-blocked taps in k_inverse_multi
   bool no_sweep = false;   // VW_NO_SWEEP: no column sweeps for deep levels
   int sweep_qc = kSweepChunk;  // VW_SWEEP_QC: q-chunk per sweep thread
+  int unroll_max = kMaxTaps;   // VW_UNROLL_MAX: longest filter that runs the tap-unrolled fused kernels
+  int blk = 10;                // VW_BLK: shortest filter that runs the register-blocked PERIODIC kernels (0 = off)
 };
 
 // One switch of the Tuning struct by its environment name; value < 0 = the default.  Returns false
@@ -98,13 +100,16 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_MULTI_RBLK") t.multi_rblk = v < 0 ? d.multi_rblk : v;
   else if (k == "VW_NO_SWEEP") t.no_sweep = v > 0;
   else if (k == "VW_SWEEP_QC") t.sweep_qc = v >= 16 ? v : d.sweep_qc;
+  else if (k == "VW_UNROLL_MAX") t.unroll_max = v < 0 ? d.unroll_max : v;
+  else if (k == "VW_BLK") t.blk = v < 0 ? d.blk : v;
   else return false;
   return true;
 }
 
 static const char* const kTuningKeys[] = {
     "VW_NV", "VW_FWD_PERSIST", "VW_FWD_BUF", "VW_FORCE_TILED", "VW_FWD_REV", "VW_INV_REV",
-    "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_NO_SWEEP", "VW_SWEEP_QC"};
+    "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_NO_SWEEP", "VW_SWEEP_QC",
+    "VW_UNROLL_MAX", "VW_BLK"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -787,7 +792,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     a.x = x; a.ldx = ldx; a.details = details; a.approx = approx; a.B = B; a.N = (int)N; a.J = J;
     a.npow2 = npow2; a.hlpad = hlpad; a.region1 = dbl ? (int)region : 0;
     a.vec_io = (ldx % V == 0) && (N % V == 0) && aligned16(x) && aligned16(details) && aligned16(approx);
-    a.unrolled = a.vec_io && fit;
+    a.unrolled = a.vec_io && fit && L <= tu.unroll_max;
     a.validate = validate; a.bad = c->bad;
     a.rev = tu.fwd_rev;
     for (int j = 0; j < J; ++j) a.hist[j] = hist ? hist[j] : nullptr;
@@ -798,9 +803,37 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     for (int j = 0; j < J; ++j) a.lv[j] = lv[j];
     if (validate) VW_HIP(hipMemsetAsync(c->bad, 0xFF, sizeof(unsigned long long), c->stream));
     const bool persist = dbl && a.unrolled && persist_ok(threads, nv, fit);
+    // register-blocked PERIODIC forward for long filters (vw_device.h k_forward_blk): padded layouts
+    int blk_lds = 0;
+    if (tu.blk > 0 && L >= tu.blk && a.unrolled && !validate && !hist && (int64_t)threads * nv == nvec) {
+      bool okb = true;
+      int hlv = 0;
+      for (int j = 0; j < J; ++j) {
+        if (lv[j].mode != kHaloPeriodic) okb = false;
+        hlv = std::max<int>(hlv, (int)(((int64_t)(L - 1) * lv[j].s + V - 1) / V));
+      }
+      const int mJ = std::max(1, lv[J - 1].s / V);
+      if (nvec % ((int64_t)nv * mJ) != 0 || hlv > nvec) okb = false;
+      int64_t buf = 0;
+      for (int j = 0; j < J && okb; ++j) {
+        int sh, pd;
+        blk_layout_host(lv[j].s / V, nv, &sh, &pd);
+        const int64_t u = hlv + nvec - 1;
+        buf = std::max(buf, u + (u >> sh) * pd + 1);
+      }
+      if (okb && buf * 16 <= kLdsBytes) {
+        const bool two = 2 * buf * 16 <= 80 * 1024;  // two buffers only where two workgroups still fit a CU
+        a.region1 = two ? (int)(buf * V) : 0;
+        a.hlpad = hlv * V;
+        a.tap_lds = (int)(buf * V * (two ? 2 : 1));
+        blk_lds = (int)(buf * 16 * (two ? 2 : 1)) + 2 * L * (int)sizeof(T);
+        if (blk_lds > kLdsBytes) blk_lds = 0;
+      }
+    }
     {
       LaunchTimer lt(c, "forward");
-      hipError_t e = persist ? launch_forward_persist<T>(a, threads, lds, fma, nv, c->stream)
+      hipError_t e = blk_lds ? launch_forward_blk<T>(a, threads, blk_lds, fma, nv, c->stream)
+                   : persist ? launch_forward_persist<T>(a, threads, lds, fma, nv, c->stream)
                              : launch_forward_fused<T>(a, threads, lds, fma, nv, c->stream);
       if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward launch failed: %s", hipGetErrorString(e));
     }
@@ -968,6 +1001,33 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     memset(&a, 0, sizeof(a));
     a.details = details; a.approx = approx; a.y = y; a.B = B; a.N = (int)N; a.J = J;
     a.db = db ? 1 : 0;
+    a.hlpad_a = hlpad; a.hlpad_d = hlpad; a.region_d = (int)region;
+    a.vec_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
+    a.unrolled = a.vec_io && fit && L <= tu.unroll_max;
+    a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.thr_ld = thr_ld; a.soft = soft; a.taps = L;
+    a.rev = tu.inv_rev;
+    // register-blocked PERIODIC inverse for long filters (vw_device.h k_inverse_blk)
+    if (tu.blk > 0 && L >= tu.blk && !pair && !db && boundary == VW_PERIODIC && a.unrolled &&
+        (int64_t)threads * nv == nvec) {
+      bool okb = true;
+      int64_t buf = 0;
+      const int mJ = std::max(1, lv[J - 1].s / V);
+      if (nvec % ((int64_t)nv * mJ) != 0) okb = false;
+      for (int j = 0; j < J && okb; ++j) {
+        if (lv[j].dir_a != 1 || lv[j].dir_d != 1 || lv[j].off_a != 0 || lv[j].off_d != 0) okb = false;
+        const int64_t hrv = ((int64_t)(L - 1) * lv[j].s + V - 1) / V;
+        if (hrv > nvec) okb = false;
+        int sh, pd;
+        blk_layout_host(lv[j].s / V, nv, &sh, &pd);
+        const int64_t u = nvec + hrv - 1;
+        buf = std::max(buf, u + (u >> sh) * pd + 1);
+      }
+      if (okb && buf * 16 + 2 * L * (int64_t)sizeof(T) <= kLdsBytes) {
+        a.blk = 1;
+        a.tap_lds = (int)(buf * V);
+        lds = (int)(buf * 16) + 2 * L * (int)sizeof(T);
+      }
+    }
     copy_taps(a.lo, lo, L);
     copy_taps(a.hi, hi, L);
     for (int j = 0; j < J; ++j) a.lv[j] = lv[j];

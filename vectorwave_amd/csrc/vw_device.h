@@ -26,6 +26,7 @@
 //  * Bandwidth-bound stencil: no MFMA.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 #include "vw_internal.h"
 
 #pragma clang fp contract(off)
@@ -120,6 +121,21 @@ __device__ __forceinline__ void fill_halo(T* buf, int N, int hl, int hr, int mod
 }
 
 // ---------------------------------------------------------------------------------------------
+// Register windows of the levels whose spacing is below the vector width.  Long filters take their
+// taps in chunks of kWinTaps, each with its own aligned sub-window (a whole-filter window of coif5
+// at spacing 2 in fp32 would be 64 registers); per output the taps still ascend.
+constexpr int kWinTaps = 8;
+
+__host__ __device__ constexpr int floor_div(int a, int b) { return a >= 0 ? a / b : -((-a + b - 1) / b); }
+
+template <int C, int NC, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (C < NC) {
+    f(std::integral_constant<int, C>{});
+    static_for<C + 1, NC>(f);
+  }
+}
+
 // Forward: one 16-byte vector of consecutive outputs t0..t0+V-1, both filters from one set of
 // LDS reads.  acc_e (+)= x[t0 + e - i*s] * f[i], i ascending (ScalarOps.java:707-719 order).
 template <typename T, int L, bool FMA, int S>
@@ -127,24 +143,32 @@ __device__ __forceinline__ void fwd_window(const T* buf, int t0, const T* lo, co
                                            T (&al)[VT<T>::V], T (&ah)[VT<T>::V]) {
   constexpr int V = VT<T>::V;
   using vec = typename VT<T>::v;
-  constexpr int RU = (((L - 1) * S) + V - 1) / V * V;   // aligned left reach
-  constexpr int NE = RU + V;
-  T w[NE];
+  static_for<0, (L + kWinTaps - 1) / kWinTaps>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * kWinTaps;
+    constexpr int I1 = (I0 + kWinTaps < L) ? I0 + kWinTaps : L;
+    constexpr int A = floor_div(-(I1 - 1) * S, V) * V;       // offsets e - i*S, aligned down
+    constexpr int E = (floor_div(V - 1 - I0 * S, V) + 1) * V;
+    constexpr int NE = E - A;
+    T w[NE];
 #pragma unroll
-  for (int k = 0; k < NE / V; ++k) {
-    vec v = *reinterpret_cast<const vec*>(buf + t0 - RU + k * V);
+    for (int k = 0; k < NE / V; ++k) {
+      vec v = *reinterpret_cast<const vec*>(buf + t0 + A + k * V);
 #pragma unroll
-    for (int e = 0; e < V; ++e) w[k * V + e] = v[e];
-  }
-#pragma unroll
-  for (int i = 0; i < L; ++i) {
-#pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const T xv = w[RU + e - i * S];
-      al[e] = madd<FMA>(al[e], xv, lo[i]);
-      ah[e] = madd<FMA>(ah[e], xv, hi[i]);
+      for (int e = 0; e < V; ++e) w[k * V + e] = v[e];
     }
-  }
+    T fl[I1 - I0], fh[I1 - I0];
+#pragma unroll
+    for (int i = I0; i < I1; ++i) { fl[i - I0] = lo[i]; fh[i - I0] = hi[i]; }
+#pragma unroll
+    for (int i = I0; i < I1; ++i) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        const T xv = w[e - i * S - A];
+        al[e] = madd<FMA>(al[e], xv, fl[i - I0]);
+        ah[e] = madd<FMA>(ah[e], xv, fh[i - I0]);
+      }
+    }
+  });
 }
 
 template <typename T, int L, bool FMA>
@@ -186,26 +210,29 @@ template <typename T, int L, bool FMA, int S, int DIR>
 __device__ __forceinline__ void inv_window(const T* buf, int base, const T* f, T (&acc)[VT<T>::V]) {
   constexpr int V = VT<T>::V;
   using vec = typename VT<T>::v;
-  // DIR=+1: elements [base, base + V-1 + (L-1)S]; DIR=-1: [base - (L-1)S, base + V-1]
-  constexpr int REACH = (L - 1) * S;
-  constexpr int RU = (REACH + V - 1) / V * V;
-  constexpr int NE = RU + V;
-  T w[NE];
-  const int start = DIR > 0 ? base : base - RU;
+  static_for<0, (L + kWinTaps - 1) / kWinTaps>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * kWinTaps;
+    constexpr int I1 = (I0 + kWinTaps < L) ? I0 + kWinTaps : L;
+    // offsets e + DIR*i*S of the chunk's taps, aligned to whole vectors
+    constexpr int A = DIR > 0 ? floor_div(I0 * S, V) * V : floor_div(-(I1 - 1) * S, V) * V;
+    constexpr int E = DIR > 0 ? (floor_div(V - 1 + (I1 - 1) * S, V) + 1) * V : (floor_div(V - 1 - I0 * S, V) + 1) * V;
+    constexpr int NE = E - A;
+    T w[NE];
 #pragma unroll
-  for (int k = 0; k < NE / V; ++k) {
-    vec v = *reinterpret_cast<const vec*>(buf + start + k * V);
+    for (int k = 0; k < NE / V; ++k) {
+      vec v = *reinterpret_cast<const vec*>(buf + base + A + k * V);
 #pragma unroll
-    for (int e = 0; e < V; ++e) w[k * V + e] = v[e];
-  }
-#pragma unroll
-  for (int i = 0; i < L; ++i) {
-#pragma unroll
-    for (int e = 0; e < V; ++e) {
-      const T xv = DIR > 0 ? w[e + i * S] : w[RU + e - i * S];
-      acc[e] = madd<FMA>(acc[e], xv, f[i]);
+      for (int e = 0; e < V; ++e) w[k * V + e] = v[e];
     }
-  }
+    T fc[I1 - I0];
+#pragma unroll
+    for (int i = I0; i < I1; ++i) fc[i - I0] = f[i];
+#pragma unroll
+    for (int i = I0; i < I1; ++i) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = madd<FMA>(acc[e], w[e + DIR * i * S - A], fc[i - I0]);
+    }
+  });
 }
 
 template <typename T, int L, bool FMA>
@@ -957,6 +984,301 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_seq(const InvArg
     }
   }
   for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, w * V, N, vec_ok, acc[k]); });
+}
+
+// ---------------------------------------------------------------------------------------------
+// Register-blocked PERIODIC kernels for long filters (L > 8: sym8, coif5, ...).  At a level with
+// spacing s >= V (vector stride m = s/V) a thread owns the NV output vectors vb, vb+m, .., vb+(NV-1)m
+// of a block of m columns; they read the same input vectors shifted by one tap, so a branch costs
+// NV+L-1 LDS reads instead of NV*L (33 vs 120 at L = 30): the per-level LDS read traffic, which bounds
+// the one-vector-per-tap kernels for long filters, drops ~3.6x.  The block mapping alone would put
+// 4..16 lanes of one ds_read_b128 lane group on the same banks, so every level input is written into
+// LDS in a padded layout chosen for that level -- NV = 4: one pad vector per 4 (m <= 4), two per 8
+// (m = 8); NV = 8: one per 8 (m <= 8); none for m >= 16 -- under which the reads are conflict-free
+// (modelled with the gfx950 lane groups of the microarchitecture guide's LDS table).  Levels with
+// s < V run the register-window code in the standard mapping.  Per output the taps run i ascending
+// (forward: ScalarOps.java:707-719; inverse: approximation branch then detail branch,
+// MultiLevelMODWTTransform.java:576-589): the reference's sums bit for bit in EXACT mode.
+struct BlkLayout {
+  int sh, pad;  // logical vector u -> u + (u >> sh) * pad
+};
+
+__device__ __forceinline__ BlkLayout blk_layout(int m, int nv) {
+  if (m <= 0 || m >= 16) return BlkLayout{30, 0};
+  if (nv >= 8) return BlkLayout{3, 1};
+  if (m == 8) return BlkLayout{3, 2};
+  return BlkLayout{2, 1};
+}
+
+__device__ __forceinline__ int blk_phys(const BlkLayout& lo, int u) { return u + (u >> lo.sh) * lo.pad; }
+
+template <typename T>
+__device__ __forceinline__ void blk_store(T* R, const BlkLayout& lo, int u, const typename VT<T>::v& o) {
+  *reinterpret_cast<typename VT<T>::v*>(R + blk_phys(lo, u) * VT<T>::V) = o;
+}
+
+// thread tid's block base at vector stride m (NV vectors per column)
+template <int NV>
+__device__ __forceinline__ int blk_base(int m) {
+  const int tid = threadIdx.x;
+  return (tid / m) * (m * NV) + tid % m;
+}
+
+// One branch of the inverse (reads t + i*s): acc[r] (+)= f[i] * in[vb + (r+i)m], i ascending per r.
+// Taps in chunks of kWinTaps (each re-read at its start): NV+TC-1 reads per chunk, the chunk's taps
+// the only ones live.
+template <typename T, int L, bool FMA, int NV>
+__device__ __forceinline__ void blk_inv_branch(const T* R, const BlkLayout& lo, int vb, int m, const T* f,
+                                               T (&acc)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  static_for<0, (L + kWinTaps - 1) / kWinTaps>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * kWinTaps;
+    constexpr int I1 = (I0 + kWinTaps < L) ? I0 + kWinTaps : L;
+    T fc[I1 - I0];
+#pragma unroll
+    for (int i = I0; i < I1; ++i) fc[i - I0] = f[i];
+#pragma unroll
+    for (int q = I0; q < I1 + NV - 1; ++q) {
+      const vec x = *reinterpret_cast<const vec*>(R + blk_phys(lo, vb + q * m) * V);
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        const int i = q - r;
+        if (i >= I0 && i < I1) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) acc[r][e] = madd<FMA>(acc[r][e], x[e], fc[i - I0]);
+        }
+      }
+      if (((q - I0) & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight
+    }
+  });
+#pragma unroll
+  for (int r = 0; r < NV; ++r)
+#pragma unroll
+    for (int e = 0; e < V; ++e) asm volatile("" : "+v"(acc[r][e]));  // pin the sums (see inv_row_t)
+}
+
+// The forward (reads t - i*s, both filters from one set of reads): within a tap chunk q runs down so
+// that for every output r the tap i = r - q ascends; chunks ascend.  Input vector u sits at logical
+// u + HLV.
+template <typename T, int L, bool FMA, int NV>
+__device__ __forceinline__ void blk_fwd(const T* X, const BlkLayout& lo, int HLV, int vb, int m, const T* flo,
+                                        const T* fhi, T (&al)[NV][VT<T>::V], T (&ah)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+#pragma unroll
+  for (int r = 0; r < NV; ++r)
+#pragma unroll
+    for (int e = 0; e < V; ++e) { al[r][e] = T(0); ah[r][e] = T(0); }
+  static_for<0, (L + kWinTaps - 1) / kWinTaps>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * kWinTaps;
+    constexpr int I1 = (I0 + kWinTaps < L) ? I0 + kWinTaps : L;
+    T fl[I1 - I0], fh[I1 - I0];
+#pragma unroll
+    for (int i = I0; i < I1; ++i) { fl[i - I0] = flo[i]; fh[i - I0] = fhi[i]; }
+#pragma unroll
+    for (int q = NV - 1 - I0; q > -I1; --q) {
+      const vec x = *reinterpret_cast<const vec*>(X + blk_phys(lo, vb + q * m + HLV) * V);
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        const int i = r - q;
+        if (i >= I0 && i < I1) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            al[r][e] = madd<FMA>(al[r][e], x[e], fl[i - I0]);
+            ah[r][e] = madd<FMA>(ah[r][e], x[e], fh[i - I0]);
+          }
+        }
+      }
+      if (((NV - 1 - I0 - q) & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+#pragma unroll
+  for (int r = 0; r < NV; ++r)
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      asm volatile("" : "+v"(al[r][e]));
+      asm volatile("" : "+v"(ah[r][e]));
+    }
+}
+
+// Forward, PERIODIC, one signal per workgroup: MultiLevelMODWTTransform.decompose (:243-251) /
+// BatchSIMDMODWT.batchMultiLevelMODWTSoA (:362-377) / VectorWaveSwtAdapter forward.  Level inputs in
+// one LDS buffer (p.region1 == 0: two barriers per level) or two (one barrier).  Left wrap images:
+// element t is also the value at t - N.  Host contract: unrolled (L > 0), aligned rows, nvec =
+// threads * NV, nvec a multiple of NV * m_J, no validation / history, p.hlpad = HLV * V.
+template <typename T, int L, bool FMA, int NV>
+__global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* X = reinterpret_cast<T*>(smem);
+  T* Y = p.region1 ? X + p.region1 : X;
+  const bool dbl = p.region1 != 0;
+  const long long b = blockIdx.x;
+  // the taps live in LDS (p.tap_lds): read per level and chunk, never hoisted out of the level loop --
+  // all 2L taps of a long filter held in registers across it spill (60 for coif5)
+  T* const taps = reinterpret_cast<T*>(smem) + p.tap_lds;
+  if (threadIdx.x < 2 * L) taps[threadIdx.x] = threadIdx.x < L ? p.lo[threadIdx.x] : p.hi[threadIdx.x - L];
+  const T* const flo = taps;
+  const T* const fhi = taps + L;
+  const int N = p.N;
+  const int nvec = N / V;
+  const int NT = blockDim.x;
+  const int tid = threadIdx.x;
+  const int HLV = p.hlpad / V;
+  auto m_of = [&](int j) { return p.lv[j - 1].s / V; };
+  auto hlv_of = [&](int j) { return ((L - 1) * p.lv[j - 1].s + V - 1) / V; };
+  // vector w of level j's input (+ its left wrap image)
+  auto put = [&](T* buf, int j, int w, const vec& o) {
+    const BlkLayout lo = blk_layout(m_of(j), NV);
+    blk_store<T>(buf, lo, w + HLV, o);
+    if (w >= nvec - hlv_of(j)) blk_store<T>(buf, lo, w - nvec + HLV, o);
+  };
+  {
+    T r0[NV][V];
+    load_row_regs<T, NV>(r0, p.x + b * p.ldx, N, nvec, true, false);
+    wait_vmem();
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      int w = tid + k * NT;
+      asm volatile("" : "+v"(w));
+      vec o;
+#pragma unroll
+      for (int e = 0; e < V; ++e) o[e] = r0[k][e];
+      put(X, 1, w, o);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  for (int j = 1; j <= p.J; ++j) {
+    const int m = m_of(j);
+    lds_barrier();  // X = level input + images; every read of Y (previous level) done
+    T* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
+    T* aout = p.approx + b * (size_t)N;
+    const bool last = j == p.J;
+    T al[NV][V], ah[NV][V];
+    int vb = 0;
+    if (m) {
+      vb = blk_base<NV>(m);
+      blk_fwd<T, L, FMA, NV>(X, blk_layout(m, NV), HLV, vb, m, flo, fhi, al, ah);
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        store_vec<VW_FWD_STORE_AUX>(dout, (vb + r * m) * V, N, true, ah[r]);
+        if (last) store_vec<VW_FWD_STORE_AUX>(aout, (vb + r * m) * V, N, true, al[r]);
+      }
+    } else {
+      fwd_row<T, L, FMA, NV>(X + HLV * V, nvec, p.lv[j - 1].s, flo, fhi, p.taps,
+                             [&](int k, int w, const T (&l)[V], const T (&h)[V]) {
+                               store_vec<VW_FWD_STORE_AUX>(dout, w * V, N, true, h);
+                               if (last) store_vec<VW_FWD_STORE_AUX>(aout, w * V, N, true, l);
+#pragma unroll
+                               for (int e = 0; e < V; ++e) { al[k][e] = l[e]; ah[k][e] = h[e]; }
+                             });
+    }
+    if (!last) {
+      if (!dbl) lds_barrier();  // one buffer: every read of this level's input done first
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        int w = m ? vb + r * m : tid + r * NT;
+        asm volatile("" : "+v"(w));
+        vec o;
+#pragma unroll
+        for (int e = 0; e < V; ++e) o[e] = al[r][e];
+        put(Y, j + 1, w, o);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      T* t = X; X = Y; Y = t;
+    }
+  }
+}
+
+// Inverse, PERIODIC, sequential sums (K4), one region time-shared as k_inverse_seq.  Right wrap
+// images: element t is also the value at t + N.  Host contract as k_forward_blk (hlpad = 0).
+template <typename T, int L, bool FMA, int NV>
+__global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_blk(const InvArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* R = reinterpret_cast<T*>(smem);
+  const long long b = p.rev ? p.B - 1 - (long long)blockIdx.x : (long long)blockIdx.x;
+  const int N = p.N;
+  const int nvec = N / V;
+  const int NT = blockDim.x;
+  const int tid = threadIdx.x;
+  T* const taps = reinterpret_cast<T*>(smem) + p.tap_lds;  // as k_forward_blk
+  if (tid < 2 * L) taps[tid] = tid < L ? p.lo[tid] : p.hi[tid - L];
+  const T* const flo = taps;
+  const T* const fhi = taps + L;
+  auto thr_of = [&](int j) { return p.thr ? load_uniform(p.thr + (size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b) : T(0); };
+  const size_t plane = (size_t)p.B * (size_t)N;
+  auto m_of = [&](int j) { return p.lv[j - 1].s / V; };
+  auto hrv_of = [&](int j) { return ((L - 1) * p.lv[j - 1].s + V - 1) / V; };
+  auto put = [&](int j, int w, const vec& o) {
+    const BlkLayout lo = blk_layout(m_of(j), NV);
+    blk_store<T>(R, lo, w, o);
+    if (w < hrv_of(j)) blk_store<T>(R, lo, w + nvec, o);
+  };
+  // a row held in the standard mapping (w = tid + k*NT) into level j's layout; MODE as regs_to_level_m
+  auto stage_std = [&](const T (&r)[NV][V], int j, int mode, T thr_b) {
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      int w = tid + k * NT;
+      asm volatile("" : "+v"(w));
+      vec o;
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        if (mode == 1) o[e] = T(0);
+        else if (mode == 2) o[e] = threshold_t(r[k][e], thr_b, p.soft);
+        else o[e] = r[k][e];
+      }
+      put(j, w, o);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  T acc[NV][V];
+  T dreg[NV][V];
+  load_row_regs<T, NV>(acc, p.approx + b * (size_t)N, N, nvec, true, p.approx_zero != 0);
+  load_row_regs<T, NV>(dreg, p.details + (size_t)(p.J - 1) * plane + b * (size_t)N, N, nvec, true,
+                       p.lv[p.J - 1].use_d == 0);
+  wait_vmem();
+  stage_std(acc, p.J, p.approx_zero ? 1 : 0, T(0));
+
+  for (int j = p.J; j >= 1; --j) {
+    const LevelDesc lv = p.lv[j - 1];
+    const int m = m_of(j);
+    const BlkLayout lo = blk_layout(m, NV);
+    const int vb = m ? blk_base<NV>(m) : 0;
+    lds_barrier();  // R = a_j + wrap images
+    zero_regs<T, NV>(acc);
+    if (m) blk_inv_branch<T, L, FMA, NV>(R, lo, vb, m, flo, acc);
+    else inv_row<T, L, FMA, NV>(R, nvec, lv.s, 1, 0, flo, p.taps, acc);
+    lds_barrier();  // every approximation-branch read done
+    wait_vmem();    // the d_j prefetch
+    stage_std(dreg, j, lv.use_d == 0 ? 1 : (p.thr ? 2 : 0), thr_of(j));
+    if (j > 1)
+      load_row_regs<T, NV>(dreg, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, true,
+                           p.lv[j - 2].use_d == 0);
+    lds_barrier();  // R = d_j + wrap images
+    if (m) blk_inv_branch<T, L, FMA, NV>(R, lo, vb, m, fhi, acc);
+    else inv_row<T, L, FMA, NV>(R, nvec, lv.s, 1, 0, fhi, p.taps, acc);
+    if (j > 1) {
+      lds_barrier();  // every detail-branch read done
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        int w = m ? vb + r * m : tid + r * NT;
+        asm volatile("" : "+v"(w));
+        vec o;
+#pragma unroll
+        for (int e = 0; e < V; ++e) o[e] = acc[r][e];
+        put(j - 1, w, o);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  }
+  // level 1 (s = 1 < V) ran in the standard mapping: coalesced stores
+#pragma unroll
+  for (int k = 0; k < NV; ++k) store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, (tid + k * NT) * V, N, true, acc[k]);
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -32,6 +32,33 @@ hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds, bool 
   }
 }
 template hipError_t launch_forward_fused<VW_T>(const FwdArgs<VW_T>&, int, int, bool, int, hipStream_t);
+// Register-blocked PERIODIC forward (k_forward_blk), unrolled tap counts only.
+template <typename T, int L, bool FMA, int NV>
+static hipError_t run_forward_blk_nv(const FwdArgs<T>& a, int threads, int lds, hipStream_t st) {
+  auto k = k_forward_blk<T, L, FMA, NV>;
+  static int configured = 64 * 1024;
+  hipError_t e = set_lds(k, lds, &configured);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(threads), lds, st, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_forward_blk(const FwdArgs<T>& a, int threads, int lds, bool fma, int nv, hipStream_t st) {
+  switch (a.taps) {
+#define VW_CASE(n)                                                                                       \
+    case n:                                                                                              \
+      if (nv <= 4) return fma ? run_forward_blk_nv<T, n, true, 4>(a, threads, lds, st)                  \
+                              : run_forward_blk_nv<T, n, false, 4>(a, threads, lds, st);                 \
+      return fma ? run_forward_blk_nv<T, n, true, 8>(a, threads, lds, st) : run_forward_blk_nv<T, n, false, 8>(a, threads, lds, st);
+    VW_TAP_LIST(VW_CASE)
+#undef VW_CASE
+    default:
+      return hipErrorNotSupported;
+  }
+}
+template hipError_t launch_forward_blk<VW_T>(const FwdArgs<VW_T>&, int, int, bool, int, hipStream_t);
+
 // Persistent forward (k_forward_persist): as many workgroups as are resident at once, each walking
 // signals blockIdx.x + k*gridDim.x.  The resident count comes from the occupancy API (LDS-bound).
 template <typename T, int L, bool FMA, int NV>

@@ -61,6 +61,7 @@ struct FwdArgs {
   T* hist[kMaxLevels];
   int hist_update;      // 1: write the new history after each level
   int taps;             // L (runtime copy; kernels are also templated on it)
+  int tap_lds;          // k_forward_blk: element offset of the LDS tap table
   T lo[kMaxTaps];       // base taps * 1/sqrt(2)  (ScalarOps.java:909-916: same at every level)
   T hi[kMaxTaps];
   LevelDesc lv[kMaxLevels];
@@ -80,12 +81,14 @@ struct InvArgs {
   int pair;             // 1: sum += (h*a + g*d) per tap (MODWTTransform.inverse, ZERO multi-level)
   int unrolled;
   int db;               // sequential sum: 1 = two LDS buffers (k_inverse_db), 0 = one (k_inverse_seq)
+  int blk;              // 1: register-blocked PERIODIC inverse (k_inverse_blk), padded LDS layouts
   int approx_zero;
   int rev;              // 1: workgroup g owns signal B-1-g
   const T* thr;         // thresholds [J][thr_ld] (nullptr = no thresholding)
   long long thr_ld;     // level stride of thr (0: one threshold per signal for every level)
   int soft;
   int taps;
+  int tap_lds;          // k_inverse_blk: element offset of the LDS tap table
   T lo[kMaxTaps];
   T hi[kMaxTaps];
   LevelDesc lv[kMaxLevels];
@@ -166,6 +169,8 @@ hipError_t launch_forward_fused(const FwdArgs<T>& a, int threads, int lds_bytes,
 template <typename T>
 hipError_t launch_forward_persist(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
 template <typename T>
+hipError_t launch_forward_blk(const FwdArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
+template <typename T>
 hipError_t launch_inverse_fused(const InvArgs<T>& a, int threads, int lds_bytes, bool fma, int nv, hipStream_t st);
 template <typename T>
 hipError_t launch_forward_level(const LevelArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
@@ -196,6 +201,15 @@ hipError_t launch_fill_uniform(T* x, long long count, unsigned long long seed, l
 template <typename T>
 hipError_t launch_single_haar_batch(const T* x, long long ldx, long long B, int N, T* approx, T* detail,
                                     hipStream_t st);
+
+// Register-blocked kernels (k_forward_blk / k_inverse_blk): padded LDS layout of a level with vector
+// stride m (must match vw_device.h blk_layout).  Returns (shift, pad): u -> u + (u >> shift) * pad.
+inline void blk_layout_host(int m, int nv, int* sh, int* pad) {
+  if (m <= 0 || m >= 16) { *sh = 30; *pad = 0; }
+  else if (nv >= 8) { *sh = 3; *pad = 1; }
+  else if (m == 8) { *sh = 3; *pad = 2; }
+  else { *sh = 2; *pad = 1; }
+}
 
 // Which compile-time tap counts have unrolled kernels; others use the runtime-L kernel.
 bool has_unrolled_taps(int L);

@@ -7,9 +7,13 @@ namespace vw {
 template <typename T, int L, bool FMA, int NV>
 static hipError_t run_inverse_fused_nv(const InvArgs<T>& a, int threads, int lds, hipStream_t st) {
   // pairwise sums: k_inverse_fused; sequential sums: two LDS buffers (k_inverse_db) or one (k_inverse_seq)
-  static int configured_pair = 64 * 1024, configured_seq = 64 * 1024, configured_db = 64 * 1024;
-  auto k = a.pair ? k_inverse_fused<T, L, FMA, NV> : a.db ? k_inverse_db<T, L, FMA, NV> : k_inverse_seq<T, L, FMA, NV>;
-  hipError_t e = set_lds(k, lds, a.pair ? &configured_pair : a.db ? &configured_db : &configured_seq);
+  static int configured_pair = 64 * 1024, configured_seq = 64 * 1024, configured_db = 64 * 1024,
+             configured_blk = 64 * 1024;
+  const bool blk = L > 0 && a.blk && !a.pair && !a.db;  // register-blocked PERIODIC (host contract)
+  auto k = a.pair ? k_inverse_fused<T, L, FMA, NV> : a.db ? k_inverse_db<T, L, FMA, NV>
+         : blk    ? k_inverse_blk<T, (L > 0 ? L : 2), FMA, NV> : k_inverse_seq<T, L, FMA, NV>;
+  hipError_t e = set_lds(k, lds, a.pair ? &configured_pair : a.db ? &configured_db
+                                 : blk ? &configured_blk : &configured_seq);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(threads), lds, st, a);
   return hipGetLastError();
