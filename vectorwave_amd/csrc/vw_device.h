@@ -1119,7 +1119,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
   // the taps live in LDS (p.tap_lds): read per level and chunk, never hoisted out of the level loop --
   // all 2L taps of a long filter held in registers across it spill (60 for coif5)
   T* const taps = reinterpret_cast<T*>(smem) + p.tap_lds;
-  if (threadIdx.x < 2 * L) taps[threadIdx.x] = threadIdx.x < L ? p.lo[threadIdx.x] : p.hi[threadIdx.x - L];
+  for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) taps[i] = i < L ? p.lo[i] : p.hi[i - L];
   const T* const flo = taps;
   const T* const fhi = taps + L;
   const int N = p.N;
@@ -1206,7 +1206,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_blk(const InvArg
   const int NT = blockDim.x;
   const int tid = threadIdx.x;
   T* const taps = reinterpret_cast<T*>(smem) + p.tap_lds;  // as k_forward_blk
-  if (tid < 2 * L) taps[tid] = tid < L ? p.lo[tid] : p.hi[tid - L];
+  for (int i = tid; i < 2 * L; i += NT) taps[i] = i < L ? p.lo[i] : p.hi[i - L];
   const T* const flo = taps;
   const T* const fhi = taps + L;
   auto thr_of = [&](int j) { return p.thr ? load_uniform(p.thr + (size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b) : T(0); };
