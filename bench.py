@@ -288,7 +288,7 @@ def measure(torch, dist, world, eng, wl, flags, mode, steps, warmup, settle_s, e
 def max_over_ranks(torch, dist, world, v, dev):
     if world == 1:
         return v
-    t = torch.tensor([v], dtype=torch.float64, device=dev)
+    t = torch.tensor([v], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return t.item()
 
@@ -311,10 +311,15 @@ def run(args, world, rank, local):
     import torch
     import torch.distributed as dist
 
+    # VW_BENCH_DEVICE_MOD (rehearsal only): map ranks onto fewer GPUs (rank r -> r mod M)
+    dmod = int(os.environ.get("VW_BENCH_DEVICE_MOD", "0"))
+    local = local % dmod if dmod > 0 else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        # the only collectives are the timing barrier and the max over ranks of the elapsed time (host
+        # scalars, after a device synchronize): gloo -- no data-path exchange exists, so no RCCL
+        dist.init_process_group("gloo")
 
     import vectorwave_amd as vw
     from vectorwave_amd import _native as nat
@@ -354,7 +359,7 @@ def run(args, world, rank, local):
     if pass_ms:
         dom = max(pass_ms, key=lambda f: pass_ms[f])
         achieved = pass_bytes[dom] / (pass_ms[dom] * 1e-3) / 1e9
-        traffic, tsrc = committed_traffic(args.config, dom)
+        traffic, tsrc = committed_traffic(args.config, dom, rows)
         members = [f"{m} x{kernels[m]['launches_per_step']:g}" for m in PASS_FAMILIES[dom] if m in kernels]
         roof = {"bound": "hbm", "kernel": f"{dom} pass ({', '.join(members)} launches per step)",
                 "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -430,7 +435,7 @@ def run(args, world, rank, local):
         dist.destroy_process_group()
 
 
-def committed_traffic(config, fam):
+def committed_traffic(config, fam, rows=0):
     """HBM bytes per pass from the committed rocprofv3 PMC capture (FETCH_SIZE x2 + WRITE_SIZE, gfx950
     correction), with the commit it was captured at -- PMC needs its own rocprofv3 pass."""
     path = os.path.join(ROOT, "profiles", f"hbm_traffic_{config}.json")
@@ -441,6 +446,8 @@ def committed_traffic(config, fam):
             tj = json.load(fh)
         ent = tj.get(fam) or {}
         b = ent.get("bytes_per_launch")
+        if b is not None and tj.get("rows") and rows:
+            b = round(b * rows / tj["rows"])  # captured on the full batch; this rank's share
         src = f"profiles/hbm_traffic_{config}.json (rocprofv3 PMC, captured at {tj.get('captured_at', '?')})"
         return b, (src if b is not None else None)
     except Exception:
