@@ -223,6 +223,20 @@ VW_API vw_status vw_noise_sigma_f64(vw_ctx *ctx, const double *coeffs, int64_t B
 VW_API vw_status vw_threshold_f64(vw_ctx *ctx, double *c, int64_t B, int64_t N, const double *thr,
                                   int soft, unsigned flags);
 
+/* ---- MODWTStreamingDenoiser statistics (device pointers only) ------------ */
+/* core/modwt/streaming/MODWTStreamingDenoiser.java:133-272 with core/util/MathUtils.java:94-257.
+ * median_out[b] = median(|x[b][:] - center[b]|) (center NULL: median(|x[b][:]|)), exact order
+ * statistics, even N = mean of the middle pair (MathUtils.median); the two passes of
+ * medianAbsoluteDeviation on non-negative data.  center requires N <= 16384. */
+VW_API vw_status vw_median_f64(vw_ctx *ctx, const double *x, int64_t B, int64_t N, const double *center,
+                               unsigned flags, double *median_out);
+/* out[0] = MathUtils.standardDeviation(x[0..N)) -- sequential sums, sqrt(ssd / (N-1)); N >= 2. */
+VW_API vw_status vw_stddev_f64(vw_ctx *ctx, const double *x, int64_t N, unsigned flags, double *out);
+/* updateNoiseEstimation's ring write: window[(start+k) % wsize] = |src[idx[k]]|, k < count <= wsize;
+ * idx is a host array (the stratified sampling positions). */
+VW_API vw_status vw_window_gather_abs_f64(vw_ctx *ctx, const double *src, const int32_t *idx, int64_t count,
+                                          double *window, int64_t wsize, int64_t start);
+
 /* ---- streaming (BatchStreamingMODWT) ------------------------------------ */
 /* levels >= 1.  PERIODIC: every block independent (== vw_modwt_forward, no cap).
  * ZERO_PADDING / SYMMETRIC: per-level left history of L_j - 1 samples kept on the device. */

@@ -9,6 +9,7 @@ holds a java.util.Random restatement so tests can reproduce the reference tests'
 from __future__ import annotations
 
 import ctypes
+import math
 import os
 import subprocess
 from ctypes import POINTER, c_double, c_int, c_longlong, c_uint, c_ulonglong, c_void_p
@@ -231,6 +232,52 @@ def conv_with_history(hist, x, flo, fhi):
     return a, d
 
 
+class StreamRestatement:
+    """BatchStreamingMODWT (ext/extensions/modwt/BatchStreamingMODWT.java) for ZERO_PADDING / SYMMETRIC,
+    one signal: per-level left history of L_j - 1 samples, initialised from the first block (zeros,
+    or the half-sample mirror of the block, fillSymmetricHistoryFromSoA :326-335), convolved with the
+    level input (generalBatchMODWTSoAWithScaledFiltersAndHistory = vwo_conv_with_history), updated
+    from the level input (updateHistoryFromSoA :337-352); flushMultiLevel (:231-275) runs a synthetic
+    tail (zeros, or the last history samples reflected, buildTailFromHistorySoA :362-376) through every
+    level's history without updating it."""
+
+    def __init__(self, lo, hi, boundary: int, levels: int):
+        self.lo, self.hi = _arr(lo), _arr(hi)
+        self.boundary, self.levels = boundary, levels
+        self.flo = [upsample_scale(self.lo, j) for j in range(1, levels + 1)]
+        self.fhi = [upsample_scale(self.hi, j) for j in range(1, levels + 1)]
+        self.hist = [None] * levels
+
+    def process(self, block):
+        cur = _arr(block)
+        n = len(cur)
+        det = np.empty((self.levels, n))
+        for j in range(self.levels):
+            hl = len(self.flo[j]) - 1
+            if self.hist[j] is None:
+                if self.boundary == ZERO_PADDING:
+                    self.hist[j] = np.zeros(hl)
+                else:
+                    self.hist[j] = np.array([cur[symmetric_index(p - hl, n)] for p in range(hl)])
+            a, d = conv_with_history(self.hist[j], cur, self.flo[j], self.fhi[j])
+            det[j] = d
+            if hl > 0:  # updateHistoryFromSoA
+                self.hist[j] = cur[n - hl:].copy() if n >= hl else np.concatenate([self.hist[j][n:], cur])
+            cur = a
+        return det, cur
+
+    def flush(self, tail_len: int):
+        h0 = self.hist[0]
+        cur = np.zeros(tail_len) if self.boundary == ZERO_PADDING else \
+            np.array([h0[len(h0) - 1 - t] for t in range(tail_len)])
+        det = np.empty((self.levels, tail_len))
+        for j in range(self.levels):
+            a, d = conv_with_history(self.hist[j], cur, self.flo[j], self.fhi[j])
+            det[j] = d
+            cur = a
+        return det, cur
+
+
 def batch_fwd_inv(x: np.ndarray, lo, hi, boundary: int, levels: int, wavelet_id: int = 0):
     """Core decompose + reconstruct per row, OpenMP over rows.  Returns (y, threads)."""
     x, lo, hi = _arr(x), _arr(lo), _arr(hi)
@@ -316,3 +363,110 @@ def wavelet_denoise(x, lo, hi, boundary: int, levels: int, method: int, fixed: f
     if st != 0:
         raise OracleError(st, bad.value)
     return y, thr
+
+
+# ---- MODWTStreamingDenoiser (core/modwt/streaming/MODWTStreamingDenoiser.java) ---------------------
+def java_median(v) -> float:
+    """MathUtils.median (core/util/MathUtils.java:94-111): exact order statistic(s), even n = mean of the
+    middle pair."""
+    s = np.sort(np.asarray(v, dtype=np.float64))
+    n = len(s)
+    return float(s[n // 2]) if n % 2 == 1 else float((s[n // 2 - 1] + s[n // 2]) / 2.0)
+
+
+def java_mad_guarded(v) -> float:
+    """calculateMAD (:212-241) + MathUtils.medianAbsoluteDeviation (:121-137)."""
+    v = np.asarray(v, dtype=np.float64)
+    fin = np.isfinite(v)
+    if not fin.any() or not (v[fin] != 0.0).any():
+        return 0.0
+    m = java_median(v)
+    return java_median(np.abs(v - m))
+
+
+def java_std_guarded(v) -> float:
+    """calculateSTD (:249-270) + MathUtils.standardDeviation (:233-257), sequential sums."""
+    v = [float(t) for t in v]
+    if sum(1 for t in v if math.isfinite(t)) < 2:
+        return 0.0
+    acc = 0.0
+    for t in v:
+        acc += t
+    mean = acc / len(v)
+    ssd = 0.0
+    for t in v:
+        d = t - mean
+        ssd += d * d
+    return math.sqrt(ssd / (len(v) - 1))
+
+
+class StreamingDenoiserRestatement:
+    """MODWTStreamingDenoiser.denoise (:94-126) for one stream: noise window update (:133-206),
+    calculateThreshold (:277-326), WaveletDenoiser.denoise / denoiseFixed."""
+
+    def __init__(self, lo, hi, boundary: int, wavelet_id: int, method: int, soft: bool, mult: float,
+                 estimation: str, window: int):
+        self.lo, self.hi, self.boundary, self.wid = _arr(lo), _arr(hi), boundary, wavelet_id
+        self.method, self.soft, self.mult, self.est, self.w = method, soft, mult, estimation, window
+        self.window = np.zeros(window)
+        self.idx = 0
+        self.level = 0.0
+
+    def _positions(self, n):
+        w = self.w
+        if n <= w:
+            return list(range(n))
+        strata = min(w, 10)
+        per, extra, size = w // strata, w % strata, n // strata
+        out = []
+        for s in range(strata):
+            start = s * size
+            end = n if s == strata - 1 else (s + 1) * size
+            take = per + (1 if s < extra else 0)
+            if take > 0:
+                length = end - start
+                step = max(1, length // take)
+                i = 0
+                while i < take and len(out) < w:
+                    j = start + (i * step) % length
+                    if j < n:
+                        out.append(j)
+                    i += 1
+        rem = w - len(out)
+        if rem > 0:
+            i = max(0, n - rem)
+            while i < n and len(out) < w:
+                out.append(i)
+                i += 1
+        return out
+
+    def denoise(self, x):
+        x = _arr(x)
+        if self.est != "FIXED":
+            _, d = modwt_forward(x, self.lo, self.hi, self.boundary)
+            for j in self._positions(len(d)):
+                self.window[self.idx] = abs(d[j])
+                self.idx = (self.idx + 1) % self.w
+            if self.est == "MAD":
+                self.level = java_mad_guarded(self.window) / 0.6745
+            else:
+                self.level = java_std_guarded(self.window)
+        if abs(self.mult - 1.0) < 1e-10:
+            y, _ = wavelet_denoise(x, self.lo, self.hi, self.boundary, 0, self.method, 0.0, self.soft, self.wid)
+            return y
+        sigma = self.level
+        if sigma <= 0.0 or self.est == "FIXED":
+            _, d = modwt_forward(x, self.lo, self.hi, self.boundary)
+            sigma = java_mad_guarded(np.abs(d)) / 0.6745
+        n = len(x)
+        if self.method == UNIVERSAL:
+            t = sigma * math.sqrt(2.0 * math.log(n))
+        elif self.method == SURE:
+            t = sigma * math.sqrt(2.0 * math.log(n)) * 0.8
+        elif self.method == MINIMAX:
+            ln = math.log(n)
+            t = 0.0 if n <= 32 else sigma * (0.3936 + 0.1829 * ln) if n <= 64 else sigma * (0.4745 + 0.1148 * ln)
+        else:
+            t = sigma
+        y, _ = wavelet_denoise(x, self.lo, self.hi, self.boundary, 0, FIXED, t * self.mult, self.soft, self.wid)
+        return y

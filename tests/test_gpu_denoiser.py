@@ -10,6 +10,7 @@ import pytest
 from oracle import oracle as O
 import vectorwave_amd as vw
 from vectorwave_amd.denoise import ThresholdMethod as M, ThresholdType as TT
+from vectorwave_amd.errors import InvalidStateException
 from vectorwave_amd.wavelets import Coiflet, Daubechies, Haar, Symlet
 
 pytestmark = pytest.mark.gpu
@@ -147,3 +148,44 @@ def test_bayes_reduces_noise_variance(engine):
     x = clean + 0.5 * rng.standard_normal(n)
     y = vw.WaveletDenoiser(Haar.INSTANCE, vw.BoundaryMode.PERIODIC).denoise(x, M.BAYES)
     assert np.var(y - clean) <= np.var(x - clean) * 1.1
+
+
+# ---- MODWTStreamingDenoiser (core/modwt/streaming/MODWTStreamingDenoiser.java) ------------------------
+@pytest.mark.parametrize("est", ["MAD", "STD", "FIXED"])
+@pytest.mark.parametrize("mult", [1.0, 1.5])
+@pytest.mark.parametrize("method", ["UNIVERSAL", "MINIMAX", "SURE"])
+@pytest.mark.parametrize("blk,win", [(256, 1024), (512, 100)], ids=["window-fills", "stratified"])
+def test_streaming_denoiser_bit_exact(engine, est, mult, method, blk, win):
+    from vectorwave_amd import MODWTStreamingDenoiser as SD
+    from vectorwave_amd.denoise import ThresholdMethod, ThresholdType
+    w = vw.get_wavelet("db4")
+    m = ThresholdMethod[method]
+    sd = (SD.builder().wavelet(w).boundaryMode(vw.BoundaryMode.PERIODIC).bufferSize(blk)
+          .thresholdType(ThresholdType.SOFT).thresholdMethod(m).thresholdMultiplier(mult)
+          .noiseEstimation(SD.NoiseEstimation[est]).noiseWindowSize(win).build())
+    ref = O.StreamingDenoiserRestatement(w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC,
+                                         w.wavelet_id, int(m), True, mult, est, win)
+    got_blocks = []
+    sd.subscribe(got_blocks.append)
+    x = O.java_random_signal(blk * 4, 77) + np.sin(np.arange(blk * 4) * 0.05)
+    for k in range(4):
+        blockx = x[k * blk:(k + 1) * blk]
+        y = sd.denoise(blockx)
+        y_ref = ref.denoise(blockx)
+        np.testing.assert_array_equal(y, y_ref)
+        assert sd.getEstimatedNoiseLevel() == ref.level
+    assert sd.getSamplesProcessed() == 4 * blk and len(got_blocks) == 4
+    sd.close()
+    assert sd.isClosed()
+    with pytest.raises(InvalidStateException):
+        sd.denoise(x[:blk])
+
+
+def test_streaming_denoiser_builder_validation(engine):
+    from vectorwave_amd import MODWTStreamingDenoiser as SD
+    for bad in (lambda b: b.bufferSize(0), lambda b: b.noiseWindowSize(-1), lambda b: b.thresholdMultiplier(0),
+                lambda b: b.wavelet(None)):
+        with pytest.raises(vw.InvalidArgumentException):
+            bad(SD.builder())
+    with pytest.raises(vw.InvalidArgumentException):
+        SD.builder().build().denoise(np.zeros(0))

@@ -272,6 +272,44 @@ def test_streaming_blocks_match_whole_signal(engine, boundary, blk, J):
     st.close()
 
 
+@pytest.mark.parametrize("boundary", [O.ZERO_PADDING, O.SYMMETRIC], ids=["Z", "S"])
+@pytest.mark.parametrize("w,blk,J", [(Daubechies.DB4, 256, 3), (Symlet.SYM8, 1000, 2), (H, 64, 4),
+                                     (Daubechies.DB4, 12000, 5)], ids=["db4-256", "sym8-1000", "haar-64", "db4-12000"])
+def test_streaming_history_and_flush_values(engine, boundary, w, blk, J):
+    # BatchStreamingMODWT ZERO/SYMMETRIC: every block and the flush tail (synthetic zeros / reflected
+    # history run through every level's history) against the restatement, bit for bit; tail lengths
+    # up to getMinFlushTailLength(), single-level flush too
+    x = signals(2, blk * 3, 17)
+    st = vw.BatchStreamingMODWT(w, vw.BoundaryMode(boundary), J)
+    refs = [O.StreamRestatement(*lohi(w), boundary, J) for _ in range(2)]
+    for k in range(3):
+        out = st.processMultiLevel(x[:, k * blk:(k + 1) * blk])
+        for b in range(2):
+            d_ref, a_ref = refs[b].process(x[b, k * blk:(k + 1) * blk])
+            exact(out.detailPerLevel[:, b, :], d_ref)
+            exact(out.finalApprox[b], a_ref)
+    m = st.getMinFlushTailLength()
+    assert m == (w.filter_length - 1)
+    for tl in sorted({1, m // 2 or 1, m}):
+        tail = st.flushMultiLevel(tl)
+        for b in range(2):
+            d_ref, a_ref = refs[b].flush(tl)
+            exact(tail.detailPerLevel[:, b, :], d_ref)
+            exact(tail.finalApprox[b], a_ref)
+    with pytest.raises(vw.InvalidArgumentException):
+        st.flushMultiLevel(m + 1)
+    st.close()
+    s1 = vw.BatchStreamingMODWT(w, vw.BoundaryMode(boundary), 1)
+    r1 = O.StreamRestatement(*lohi(w), boundary, 1)
+    s1.processSingleLevel(x[:1, :blk])
+    r1.process(x[0, :blk])
+    t1 = s1.flushSingleLevel(w.filter_length - 1)
+    d_ref, a_ref = r1.flush(w.filter_length - 1)
+    exact(t1.detail[0], d_ref[0])
+    exact(t1.approx[0], a_ref)
+    s1.close()
+
+
 # ---- FMA and fp32 variants --------------------------------------------------------------------------
 def test_fma_variant_within_tolerance(engine):
     w = Daubechies.DB4
@@ -397,7 +435,7 @@ def test_multilevel_tiles_bit_exact(engine, tile):
 
 
 # ---- alternative fused inverse kernels (selected by policy or option) ------------------------------------
-@pytest.mark.parametrize("opts", [dict(VW_INV_BUF=2), dict(VW_NV=8), dict(VW_INV_BUF=2, VW_NV=8)],
+@pytest.mark.parametrize("opts", [dict(VW_INV_BUF=1), dict(VW_INV_BUF=2), dict(VW_NV=8), dict(VW_INV_BUF=1, VW_NV=8)],
                          ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
 @pytest.mark.parametrize("fma", [False, True], ids=["exact", "fma"])
 def test_inverse_kernel_variants_bit_exact(engine, opts, fma):

@@ -390,3 +390,17 @@ def test_wavelet_denoise_restatement_properties():
     assert np.array_equal(y0, O.modwt_inverse(a, d, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC))
     with pytest.raises(O.OracleError):
         O.wavelet_denoise(x, lo, hi, O.PERIODIC, 2, O.FIXED, 0.1)
+
+
+def test_stream_restatement_matches_whole_signal_zero_padding():
+    # ZERO_PADDING streaming with zero-initialised history equals the whole-signal zero-padded transform
+    # (the first block's history is zeros; later blocks carry the true left context)
+    import vectorwave_amd as vw
+    w = vw.get_wavelet("db4")
+    lo, hi = w.lowPassDecomposition(), w.highPassDecomposition()
+    x = O.java_random_signal(300, 5)
+    st = O.StreamRestatement(lo, hi, O.ZERO_PADDING, 3)
+    parts = [st.process(x[k * 100:(k + 1) * 100]) for k in range(3)]
+    d_ref, a_ref = O.decompose(x, lo, hi, O.ZERO_PADDING, 3)
+    np.testing.assert_array_equal(np.concatenate([p[0] for p in parts], axis=1), d_ref)
+    np.testing.assert_array_equal(np.concatenate([p[1] for p in parts]), a_ref)

@@ -18,7 +18,8 @@ from .modwt import (BoundaryMode, MODWTResult, MODWTTransform, MultiLevelMODWTRe
                     MutableMultiLevelMODWTResult)
 from .swt import VectorWaveSwtAdapter
 from .denoise import ThresholdMethod, ThresholdType, WaveletDenoiser
-from .streaming import MODWTStreamingTransform, MODWTStreamingTransformImpl, MultiLevelMODWTStreamingTransform
+from .streaming import (MODWTStreamingDenoiser, MODWTStreamingTransform, MODWTStreamingTransformImpl,
+                        MultiLevelMODWTStreamingTransform)
 from .batch import BatchMODWT, BatchSIMDMODWT, BatchStreamingMODWT
 from .engine import Engine, max_levels, version
 

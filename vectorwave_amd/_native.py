@@ -75,6 +75,9 @@ SIGNATURES = {
     "vw_ctx_enable_timing": (c_int, [c_void_p, c_int]),
     "vw_ctx_kernel_time": (c_int, [c_void_p, c_char_p, POINTER(c_double), POINTER(c_int64)]),
     "vw_ctx_reset_timing": (c_int, [c_void_p]),
+    "vw_median_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_uint, c_void_p]),
+    "vw_stddev_f64": (c_int, [c_void_p, c_void_p, c_int64, c_uint, c_void_p]),
+    "vw_window_gather_abs_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int64]),
     "vw_capture_begin": (c_int, [c_void_p]),
     "vw_capture_end": (c_int, [c_void_p, POINTER(c_void_p)]),
     "vw_graph_launch": (c_int, [c_void_p, c_int64]),

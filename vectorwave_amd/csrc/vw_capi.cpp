@@ -95,7 +95,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_MULTI") t.multi = v < 0 ? d.multi : v != 0;
   else if (k == "VW_MULTI_DIV") t.multi_div = v <= 0 ? d.multi_div : v;
   else if (k == "VW_MULTI_TILE") t.multi_tile = v < 0 ? 0 : v;
-  else if (k == "VW_INV_BUF") t.inv_buf = v < 0 ? 0 : v;
+  else if (k == "VW_INV_BUF") t.inv_buf = v < 0 ? 0 : v;  // 0 = policy
   else if (k == "VW_INV_TILE") t.inv_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI_RBLK") t.multi_rblk = v < 0 ? d.multi_rblk : v;
   else if (k == "VW_NO_SWEEP") t.no_sweep = v > 0;
@@ -130,6 +130,7 @@ struct vw_ctx {
   bool capturing = false;      // between vw_capture_begin / vw_capture_end
   unsigned ws_gen = 0;         // bumped when ws / ws2 move: graphs recorded before are stale
   Tuning tune;
+  int cus = 256;               // compute units of the device (small-batch policies)
   std::recursive_mutex mu;
   void* ws = nullptr;          // tiled-path ping-pong buffers
   size_t ws_bytes = 0;
@@ -367,6 +368,7 @@ extern "C" vw_status vw_ctx_create(int device, vw_ctx** out) {
   vw_ctx* c = new vw_ctx();
   c->device = device;
   c->tune = read_tuning();
+  { int n = 0; if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess && n > 0) c->cus = n; }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     delete c;
     return fail(VW_ERR_DEVICE, "hipStreamCreate failed");
@@ -986,7 +988,11 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   // (k_inverse_db, two barriers per level) because twice the workgroups fit per CU; VW_INV_BUF=2
   // selects the latter.
   const Tuning& tu = c->tune;
-  bool db = !pair && tu.inv_buf == 2;
+  // Two LDS buffers (two barriers per level, two workgroups per CU) vs one (four barriers, three per
+  // CU): with at most ~4 signals per CU the occupancy of the one-buffer kernel is not reached and the
+  // shorter per-level chain wins (measured on MI355X, db4 4096 x {512, 1024}: -3 %); VW_INV_BUF=1|2
+  // overrides.
+  bool db = !pair && (tu.inv_buf ? tu.inv_buf == 2 : B <= 4LL * c->cus);
   bool fused = false, fit = false;
   if (!tu.force_tiled) {
     if (pair || db) fused = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
@@ -1568,6 +1574,55 @@ extern "C" vw_status vw_wavelet_denoise_f64(vw_ctx* c, const double* x, int64_t 
                                 y, thresholds_out));
   if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
   return ok();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Statistics of MODWTStreamingDenoiser (core/modwt/streaming/MODWTStreamingDenoiser.java:133-272):
+// MathUtils.median / medianAbsoluteDeviation / standardDeviation on device rows, and the noise-window
+// ring update.  Device pointers only (the window lives on the device between blocks).
+extern "C" vw_status vw_median_f64(vw_ctx* c, const double* x, int64_t B, int64_t N, const double* center,
+                                   unsigned flags, double* median_out) {
+  if (!c || !x || !median_out) return fail(VW_ERR_NULL, "null argument");
+  if (B <= 0 || N <= 0) return fail(VW_ERR_EMPTY, "Array cannot be null or empty");
+  if (center && N > 16384) return fail(VW_ERR_UNSUPPORTED, "centered median supports N <= 16384");
+  if (flags & VW_FLAG_HOST_MEMORY) return fail(VW_ERR_UNSUPPORTED, "device pointers only");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  hipError_t e = launch_median(x, N, B, (int)N, center, median_out, c->stream);
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+  if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}
+
+extern "C" vw_status vw_stddev_f64(vw_ctx* c, const double* x, int64_t N, unsigned flags, double* out) {
+  if (!c || !x || !out) return fail(VW_ERR_NULL, "null argument");
+  if (N < 2) return fail(VW_ERR_ARG, "Need at least 2 values for standard deviation");
+  if (N > (1LL << 30)) return fail(VW_ERR_ARG, "too many values");
+  if (flags & VW_FLAG_HOST_MEMORY) return fail(VW_ERR_UNSUPPORTED, "device pointers only");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  hipError_t e = launch_seq_std(x, (int)N, out, c->stream);
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+  if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
+  return ok();
+}
+
+// window[(start + k) % wsize] = |src[idx[k]]| for k < count; idx is a HOST array (the stratified
+// sampling positions are integer bookkeeping, computed by the caller), staged to the device here.
+extern "C" vw_status vw_window_gather_abs_f64(vw_ctx* c, const double* src, const int32_t* idx, int64_t count,
+                                              double* window, int64_t wsize, int64_t start) {
+  if (!c || !src || !window || (count > 0 && !idx)) return fail(VW_ERR_NULL, "null argument");
+  if (wsize <= 0 || count < 0 || count > wsize || start < 0 || start >= wsize) return fail(VW_ERR_ARG, "bad window");
+  if (count == 0) return ok();
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  if (c->capturing) return fail(VW_ERR_STATE, "cannot be captured");
+  hipSetDevice(c->device);
+  Staging s(c);
+  int32_t* di = nullptr;
+  VW_TRY(s.in(idx, (size_t)count, &di));
+  hipError_t e = launch_gather_abs(src, di, (int)count, window, (int)wsize, (int)start, c->stream);
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
+  return ok();  // Staging's destructor synchronizes before freeing the index copy
 }
 
 // ------------------------------------------------------------------------------------------------

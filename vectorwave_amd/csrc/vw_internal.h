@@ -192,6 +192,12 @@ hipError_t launch_level_threshold(const double* coeffs, long long level_stride, 
                                   const DenoiseConsts& k, long long B, int levels, double* thr, hipStream_t st);
 hipError_t launch_noise_sigma(const double* coeffs, long long ld, long long B, int N, double scale_c,
                               double* sigma_out, double* thr_out, hipStream_t st);
+// Exact median of |x - center| per row (center nullptr: of |x|); N <= 16384 when center is given.
+hipError_t launch_median(const double* x, long long ld, long long B, int N, const double* center, double* median_out,
+                         hipStream_t st);
+hipError_t launch_seq_std(const double* x, int n, double* out, hipStream_t st);
+hipError_t launch_gather_abs(const double* src, const int* idx, int count, double* window, int wsize, int start,
+                             hipStream_t st);
 template <typename T>
 hipError_t launch_transpose(const T* in, long long rows, long long cols, T* out, hipStream_t st);
 template <typename T>

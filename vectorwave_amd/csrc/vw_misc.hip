@@ -49,7 +49,27 @@ hipError_t launch_history_update(const T* in, long long ld_in, const T* old_hist
 hipError_t launch_noise_sigma(const double* coeffs, long long ld, long long B, int N, double scale_c,
                               double* sigma_out, double* thr_out, hipStream_t st) {
   hipLaunchKernelGGL(k_noise_sigma, dim3((unsigned)B), dim3(kSigmaThreads), 0, st, coeffs, ld, N, scale_c, sigma_out,
-                     thr_out);
+                     thr_out, (const double*)nullptr, (double*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t launch_median(const double* x, long long ld, long long B, int N, const double* center, double* median_out,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(k_noise_sigma, dim3((unsigned)B), dim3(kSigmaThreads), 0, st, x, ld, N, 0.0, (double*)nullptr,
+                     (double*)nullptr, center, median_out);
+  return hipGetLastError();
+}
+
+hipError_t launch_seq_std(const double* x, int n, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_seq_std, dim3(1), dim3(64), 0, st, x, n, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_abs(const double* src, const int* idx, int count, double* window, int wsize, int start,
+                             hipStream_t st) {
+  if (count <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_abs, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, src, idx, count, window,
+                     wsize, start);
   return hipGetLastError();
 }
 

@@ -114,8 +114,11 @@ constexpr int kSelCand = 1024;  // a bucket this small is finished by exact rank
 // (the same as sorting); anything unusual (non-finite keys, a range too narrow to scale, no
 // convergence in 6 passes) falls back to radix_median.  Two histogram atomics per key per pass on a
 // spread-out digit, instead of eight radix passes whose first digits every key shares.
+// center (optional, [B]): the keys are |c - center[b]| (MathUtils.medianAbsoluteDeviation's second
+// pass; N <= 16384, keys in registers); median_out (optional): the raw median.
 __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __restrict__ coeffs, long long ld, int N,
-                                                               double scale_c, double* sigma_out, double* thr_out) {
+                                                               double scale_c, double* sigma_out, double* thr_out,
+                                                               const double* __restrict__ center, double* median_out) {
   __shared__ unsigned int hist[kSelBins];
   __shared__ double cand[kSelCand];
   __shared__ double red[kSigmaThreads / 64];
@@ -127,6 +130,8 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
   const double* c = coeffs + b * ld;
   const int tid = threadIdx.x;
   const bool in_regs = N <= kSigmaThreads * kSigmaKeys;
+  const double ctr = center ? center[b] : 0.0;
+  auto key_of = [&](double v) { return abs_bits(center ? v - ctr : v); };
   const long long k1 = (N % 2 == 0) ? N / 2 - 1 : N / 2, k2 = N / 2;
   unsigned long long keys[kSigmaKeys];
   double v1 = 0.0, v2 = 0.0;
@@ -139,15 +144,15 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
       for (int k = 0; k < kSigmaKeys / 2; ++k) {
         const int w = min(tid + k * kSigmaThreads, N / 2 - 1);
         const d2 v = __builtin_nontemporal_load(reinterpret_cast<const d2*>(c) + w);
-        keys[2 * k] = abs_bits(v[0]);
-        keys[2 * k + 1] = abs_bits(v[1]);
+        keys[2 * k] = key_of(v[0]);
+        keys[2 * k + 1] = key_of(v[1]);
       }
     } else {
 #pragma unroll
       for (int k = 0; k < kSigmaKeys / 2; ++k) {
         const int i = 2 * (tid + k * kSigmaThreads);
-        keys[2 * k] = i < N ? abs_bits(c[i]) : 0ull;
-        keys[2 * k + 1] = i + 1 < N ? abs_bits(c[i + 1]) : 0ull;
+        keys[2 * k] = i < N ? key_of(c[i]) : 0ull;
+        keys[2 * k + 1] = i + 1 < N ? key_of(c[i + 1]) : 0ull;
       }
     }
     // key slot 2k+e holds element 2*(tid + k*1024) + e
@@ -266,7 +271,7 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
 #pragma unroll
       for (int k = 0; k < kSigmaKeys; ++k) {
         const int i = tid + k * kSigmaThreads;
-        keys[k] = i < N ? abs_bits(c[i]) : 0ull;
+        keys[k] = i < N ? key_of(c[i]) : 0ull;
       }
     }
     radix_median(c, N, keys, in_regs, &v1, &v2);
@@ -276,6 +281,31 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
     const double sigma = median / 0.6745;
     if (sigma_out) sigma_out[b] = sigma;
     if (thr_out) thr_out[b] = sigma * scale_c;
+    if (median_out) median_out[b] = median;
+  }
+}
+
+// MathUtils.standardDeviation (core/util/MathUtils.java:233-257): sequential sum -> mean, sequential
+// sum of squared deviations, sqrt(ssd / (n - 1)).  One lane: the reference's summation order.
+__global__ void k_seq_std(const double* __restrict__ x, int n, double* out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double sum = 0.0;
+  for (int i = 0; i < n; ++i) sum += x[i];
+  const double mean = sum / n;
+  double ssd = 0.0;
+  for (int i = 0; i < n; ++i) {
+    const double d = x[i] - mean;
+    ssd += d * d;
+  }
+  out[0] = __builtin_sqrt(ssd / (n - 1));
+}
+
+// window[(start + k) % wsize] = |src[idx[k]]|, k < count (distinct ring slots: count <= wsize).
+__global__ void k_gather_abs(const double* __restrict__ src, const int* __restrict__ idx, int count,
+                             double* window, int wsize, int start) {
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < count; k += gridDim.x * blockDim.x) {
+    const double v = src[idx[k]];
+    window[(start + k) % wsize] = __builtin_fabs(v);  // Math.abs: clears the sign bit (-0.0 -> 0.0)
   }
 }
 
