@@ -42,6 +42,17 @@ def _validate_aos(signals, what: str = "signals"):
     return signals
 
 
+def _check_batch_reach(wavelet: Wavelet, n: int, levels: int) -> None:
+    """BatchSIMDMODWT.generalBatchMODWTSoAWithScaledFilters (:384-424) indexes (t - l + N) % N: with an
+    upsampled filter longer than N + 1 that index goes negative and Java throws
+    ArrayIndexOutOfBoundsException at the first such level (IndexError here, before any work)."""
+    L = len(wavelet.lowPassDecomposition())
+    for j in range(1, levels + 1):
+        Lj = (L - 1) * (1 << (j - 1)) + 1
+        if Lj > n + 1:
+            raise IndexError(f"Index {n - Lj + 1} out of bounds for length {n} (level {j} filter length {Lj})")
+
+
 @dataclass
 class SingleLevelResult:
     approx: object   # [B][N]
@@ -75,6 +86,7 @@ class BatchMODWT:
         if levels < 1:
             raise InvalidArgumentException("levels must be >= 1")
         x = _validate_aos(signals)
+        _check_batch_reach(wavelet, x.shape[1], levels)
         det, app = _engine_for(x).forward(x, wavelet.lowPassDecomposition(), wavelet.highPassDecomposition(),
                                           wavelet.wavelet_id, nat.PERIODIC, levels, nat.FLAG_FMA if fma else 0)
         return MultiLevelResult(det, app)
