@@ -74,6 +74,7 @@ struct Tuning {
   int inv_buf = 0;         // VW_INV_BUF=2: two-buffer sequential inverse (k_inverse_db)
   int inv_tile = 0;        // VW_INV_TILE: per-level inverse tile (0 = 1024)
   int multi_rblk = 1;      // VW_MULTI_RBLK: register-blocked taps in k_inverse_multi
+  int multi_pf = 1;        // VW_MULTI_PF: k_inverse_multi prefetches the next detail tile
   bool no_sweep = false;   // VW_NO_SWEEP: no column sweeps for deep levels
   int sweep_qc = kSweepChunk;  // VW_SWEEP_QC: q-chunk per sweep thread
   int unroll_max = kMaxTaps;   // VW_UNROLL_MAX: longest filter that runs the tap-unrolled fused kernels
@@ -98,6 +99,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_INV_BUF") t.inv_buf = v < 0 ? 0 : v;  // 0 = policy
   else if (k == "VW_INV_TILE") t.inv_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI_RBLK") t.multi_rblk = v < 0 ? d.multi_rblk : v;
+  else if (k == "VW_MULTI_PF") t.multi_pf = v < 0 ? d.multi_pf : v;
   else if (k == "VW_NO_SWEEP") t.no_sweep = v > 0;
   else if (k == "VW_SWEEP_QC") t.sweep_qc = v >= 16 ? v : d.sweep_qc;
   else if (k == "VW_UNROLL_MAX") t.unroll_max = v < 0 ? d.unroll_max : v;
@@ -108,7 +110,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
 
 static const char* const kTuningKeys[] = {
     "VW_NV", "VW_FWD_PERSIST", "VW_FWD_BUF", "VW_FORCE_TILED", "VW_FWD_REV", "VW_INV_REV",
-    "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_NO_SWEEP", "VW_SWEEP_QC",
+    "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_MULTI_PF", "VW_NO_SWEEP", "VW_SWEEP_QC",
     "VW_UNROLL_MAX", "VW_BLK"};
 
 static Tuning read_tuning() {
@@ -1083,6 +1085,8 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         m.vec_io = (N % V == 0) && al;
         m.soft = soft; m.taps = L;
         m.rblk = tu.multi_rblk;
+        // register prefetch of d_{j-1} while level j computes: whole vectors, every tile of the group
+        m.pf = tu.multi_pf && m.vec_io && (int64_t)(mtile + m.ext[g - 1]) / V <= (int64_t)kMultiPF * 256;
         copy_taps(m.lo, lo, L);
         copy_taps(m.hi, hi, L);
         LaunchTimer lt(c, "inverse_level");

@@ -1644,14 +1644,59 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
   const int span = (cnt + V - 1) / V * V;
   const bool vec_ok = p.vec_io != 0;
   const int top = p.nlev - 1;
+  // Detail prefetch (p.pf, host contract: whole vectors, (span + ext[top]) / V <= kMultiPF * 256): the
+  // tile of d_{k-1} is loaded into registers right after level k's first barrier and written to D
+  // after its second, so the HBM latency of the next level's input overlaps this level's arithmetic.
+  // The loads are unconditional (clamped vector index): an exec-masked load block makes the waitcnt
+  // pass wait for it at the first LDS read.
+  const bool pf = p.pf != 0;
+  vec dreg[kMultiPF];
+  auto d_load = [&](int k) {
+    const T* sd = p.src_d[k];
+    const int nvd = (span + p.ext[k]) / V;
+#pragma unroll
+    for (int i = 0; i < kMultiPF; ++i) {
+      const int w = min((int)threadIdx.x + i * 256, nvd - 1);
+      int pos = ts + w * V;
+      if (pos >= N) pos %= N;  // periodic wrap of the right reach
+      if (sd)
+        dreg[i] = __builtin_nontemporal_load(reinterpret_cast<const vec*>(sd + b * (size_t)N + pos));
+      else
+#pragma unroll
+        for (int e = 0; e < V; ++e) dreg[i][e] = T(0);
+    }
+  };
+  auto d_store = [&](int k) {
+    const T* th = p.thr[k];
+    const T thb = th ? th[b] : T(0);
+    const int nvd = (span + p.ext[k]) / V;
+#pragma unroll
+    for (int i = 0; i < kMultiPF; ++i) {
+      const int w = (int)threadIdx.x + i * 256;
+      if (w < nvd) {
+        vec v = dreg[i];
+        if (th)
+#pragma unroll
+          for (int e = 0; e < V; ++e) v[e] = threshold_t(v[e], thb, p.soft);
+        *reinterpret_cast<vec*>(D + w * V) = v;
+      }
+    }
+  };
   tile_to_lds(A, p.src_a ? p.src_a + b * (size_t)N : p.src_a, N, ts, 0, span + p.ext[top], kHaloPeriodic, 0,
               (const T*)nullptr, 0, (const T*)nullptr, T(0), 0, p.src_a == nullptr, vec_ok);
+  if (pf) {
+    d_load(top);
+    d_store(top);
+  }
   for (int k = top; k >= 0; --k) {
-    const T* sd = p.src_d[k];
-    const T* th = p.thr[k];
-    tile_to_lds(D, sd ? sd + b * (size_t)N : sd, N, ts, 0, span + p.ext[k], kHaloPeriodic, 0, (const T*)nullptr, 0,
-                th, th ? th[b] : T(0), p.soft, sd == nullptr, vec_ok);
+    if (!pf) {
+      const T* sd = p.src_d[k];
+      const T* th = p.thr[k];
+      tile_to_lds(D, sd ? sd + b * (size_t)N : sd, N, ts, 0, span + p.ext[k], kHaloPeriodic, 0, (const T*)nullptr, 0,
+                  th, th ? th[b] : T(0), p.soft, sd == nullptr, vec_ok);
+    }
     lds_barrier();  // A and D complete
+    if (pf && k > 0) d_load(k - 1);
     const int s = p.s0 << k;
     const int nv = (span + (k > 0 ? p.ext[k - 1] : 0)) / V;  // the tile + what the next levels read
     T acc[NI][V];
@@ -1705,6 +1750,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
             }
           }
         }
+        if (pf) d_store(k - 1);
         continue;
       }
     }
@@ -1733,6 +1779,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
         *reinterpret_cast<vec*>(A + w * V) = o;
       }
     }
+    if (pf) d_store(k - 1);
   }
 }
 

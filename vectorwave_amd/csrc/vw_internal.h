@@ -126,6 +126,7 @@ struct LevelArgs {
 // launch, the intermediate approximations kept in LDS (vw_device.h k_forward_multi / k_inverse_multi).
 constexpr int kMaxGroup = 8;
 constexpr int kMultiInvNI = 8;  // k_inverse_multi: output vectors per thread (256 threads)
+constexpr int kMultiPF = 6;     // k_inverse_multi: prefetched detail vectors per thread (256 threads)
 template <typename T>
 struct MultiArgs {
   const T* src_a;            // forward: input of the group's first level [B][lda]; inverse: a_{j1} [B][N] (nullptr = 0)
@@ -147,6 +148,7 @@ struct MultiArgs {
   int soft;
   int taps;
   int rblk;                  // inverse: register-blocked taps where S is a multiple of V
+  int pf;                    // inverse: next level's detail tile prefetched into registers
   T lo[kMaxTaps];
   T hi[kMaxTaps];
 };
