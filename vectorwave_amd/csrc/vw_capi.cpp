@@ -809,7 +809,9 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     const bool persist = dbl && a.unrolled && persist_ok(threads, nv, fit);
     // register-blocked PERIODIC forward for long filters (vw_device.h k_forward_blk): padded layouts
     int blk_lds = 0;
-    if (tu.blk > 0 && L >= tu.blk && a.unrolled && !validate && !hist && (int64_t)threads * nv == nvec) {
+    // (NV = 8: 1024-thread workgroups cap a lane at 128 VGPRs and the blocked forward spills there --
+    // measured 2x slower at sym8 N = 16384; the one-vector-per-tap kernel runs instead)
+    if (tu.blk > 0 && L >= tu.blk && a.unrolled && !validate && !hist && (int64_t)threads * nv == nvec && nv <= 4) {
       bool okb = true;
       int hlv = 0;
       for (int j = 0; j < J; ++j) {
@@ -818,12 +820,20 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
       }
       const int mJ = std::max(1, lv[J - 1].s / V);
       if (nvec % ((int64_t)nv * mJ) != 0 || hlv > nvec) okb = false;
-      int64_t buf = 0;
-      for (int j = 0; j < J && okb; ++j) {
-        int sh, pd;
-        blk_layout_host(lv[j].s / V, nv, &sh, &pd);
-        const int64_t u = hlv + nvec - 1;
-        buf = std::max(buf, u + (u >> sh) * pd + 1);
+      auto buf_of = [&](int tight) {
+        int64_t bf = 0;
+        for (int j = 0; j < J; ++j) {
+          int sh, pd;
+          blk_layout_host(lv[j].s / V, nv, &sh, &pd, tight);
+          const int64_t u = hlv + nvec - 1;
+          bf = std::max(bf, u + (u >> sh) * pd + 1);
+        }
+        return bf;
+      };
+      int64_t buf = buf_of(0);
+      if (buf * 16 + 2 * L * (int64_t)sizeof(T) > kLdsBytes && nv >= 8) {
+        a.blk_tight = 1;
+        buf = buf_of(1);
       }
       if (okb && buf * 16 <= kLdsBytes) {
         const bool two = 2 * buf * 16 <= 80 * 1024;  // two buffers only where two workgroups still fit a CU
@@ -1021,16 +1031,24 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       int64_t buf = 0;
       const int mJ = std::max(1, lv[J - 1].s / V);
       if (nvec % ((int64_t)nv * mJ) != 0) okb = false;
+      int64_t buf_t = 0;
       for (int j = 0; j < J && okb; ++j) {
         if (lv[j].dir_a != 1 || lv[j].dir_d != 1 || lv[j].off_a != 0 || lv[j].off_d != 0) okb = false;
         const int64_t hrv = ((int64_t)(L - 1) * lv[j].s + V - 1) / V;
         if (hrv > nvec) okb = false;
         int sh, pd;
-        blk_layout_host(lv[j].s / V, nv, &sh, &pd);
         const int64_t u = nvec + hrv - 1;
+        blk_layout_host(lv[j].s / V, nv, &sh, &pd);
         buf = std::max(buf, u + (u >> sh) * pd + 1);
+        blk_layout_host(lv[j].s / V, nv, &sh, &pd, 1);
+        buf_t = std::max(buf_t, u + (u >> sh) * pd + 1);
       }
-      if (okb && buf * 16 + 2 * L * (int64_t)sizeof(T) <= kLdsBytes) {
+      const int64_t taps_b = 2 * L * (int64_t)sizeof(T);
+      if (okb && buf * 16 + taps_b > kLdsBytes && nv >= 8 && buf_t * 16 + taps_b <= kLdsBytes) {
+        a.blk_tight = 1;  // sparse padding so the level fits (sym8 at N = 16384)
+        buf = buf_t;
+      }
+      if (okb && buf * 16 + taps_b <= kLdsBytes) {
         a.blk = 1;
         a.tap_lds = (int)(buf * V);
         lds = (int)(buf * 16) + 2 * L * (int)sizeof(T);

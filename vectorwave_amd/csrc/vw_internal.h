@@ -62,6 +62,7 @@ struct FwdArgs {
   int hist_update;      // 1: write the new history after each level
   int taps;             // L (runtime copy; kernels are also templated on it)
   int tap_lds;          // k_forward_blk: element offset of the LDS tap table
+  int blk_tight;        // k_forward_blk: sparse padding (blk_layout)
   T lo[kMaxTaps];       // base taps * 1/sqrt(2)  (ScalarOps.java:909-916: same at every level)
   T hi[kMaxTaps];
   LevelDesc lv[kMaxLevels];
@@ -89,6 +90,7 @@ struct InvArgs {
   int soft;
   int taps;
   int tap_lds;          // k_inverse_blk: element offset of the LDS tap table
+  int blk_tight;        // k_inverse_blk: sparse padding (blk_layout)
   T lo[kMaxTaps];
   T hi[kMaxTaps];
   LevelDesc lv[kMaxLevels];
@@ -212,9 +214,9 @@ hipError_t launch_single_haar_batch(const T* x, long long ldx, long long B, int 
 
 // Register-blocked kernels (k_forward_blk / k_inverse_blk): padded LDS layout of a level with vector
 // stride m (must match vw_device.h blk_layout).  Returns (shift, pad): u -> u + (u >> shift) * pad.
-inline void blk_layout_host(int m, int nv, int* sh, int* pad) {
+inline void blk_layout_host(int m, int nv, int* sh, int* pad, int tight = 0) {
   if (m <= 0 || m >= 16) { *sh = 30; *pad = 0; }
-  else if (nv >= 8) { *sh = 3; *pad = 1; }
+  else if (nv >= 8) { *sh = tight ? 4 : 3; *pad = 1; }
   else if (m == 8) { *sh = 3; *pad = 2; }
   else { *sh = 2; *pad = 1; }
 }
