@@ -11,7 +11,7 @@ fatal() { local rc=$1; [ "$rc" -ge 124 ] || [ "$rc" -eq 134 ] || [ "$rc" -eq 139
 for s in $STEPS; do
   case "$s" in
     tests)
-      timeout -k 10 ${T_TESTS:-420} python -m pytest tests -m gpu -q -x ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+      timeout -k 10 ${T_TESTS:-420} python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
       tail -5 gpurun_out/pytest_gpu.log; echo "tests rc=$rc" ;;
     smoke)
       timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
