@@ -1177,13 +1177,21 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
         if (last) store_vec<VW_FWD_STORE_AUX>(aout, (vb + r * m) * V, N, true, al[r]);
       }
     } else {
-      fwd_row<T, L, FMA, NV>(X + HLV * V, nvec, p.lv[j - 1].s, flo, fhi, p.taps,
-                             [&](int k, int w, const T (&l)[V], const T (&h)[V]) {
-                               store_vec<VW_FWD_STORE_AUX>(dout, w * V, N, true, h);
-                               if (last) store_vec<VW_FWD_STORE_AUX>(aout, w * V, N, true, l);
+      // s < V (m == 0): only the register-window forms.  (fwd_row's strided form, unreachable here,
+      // kept all 2L taps of its loop live and spilled coif5 fp32: 193 VGPRs of scratch, 1.5x the
+      // kernel's HBM write bytes -- profiles/r02/hbm_traffic_coif5-f32.json.)
+      auto em = [&](int k, int w, const T (&l)[V], const T (&h)[V]) {
+        store_vec<VW_FWD_STORE_AUX>(dout, w * V, N, true, h);
+        if (last) store_vec<VW_FWD_STORE_AUX>(aout, w * V, N, true, l);
 #pragma unroll
-                               for (int e = 0; e < V; ++e) { al[k][e] = l[e]; ah[k][e] = h[e]; }
-                             });
+        for (int e = 0; e < V; ++e) { al[k][e] = l[e]; ah[k][e] = h[e]; }
+      };
+      if constexpr (V == 4) {
+        if (p.lv[j - 1].s == 2) fwd_row_t<T, L, FMA, NV, 2>(X + HLV * V, nvec, 2, flo, fhi, p.taps, em);
+        else fwd_row_t<T, L, FMA, NV, 1>(X + HLV * V, nvec, 1, flo, fhi, p.taps, em);
+      } else {
+        fwd_row_t<T, L, FMA, NV, 1>(X + HLV * V, nvec, 1, flo, fhi, p.taps, em);
+      }
     }
     if (!last) {
       if (!dbl) lds_barrier();  // one buffer: every read of this level's input done first
