@@ -1086,10 +1086,11 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   // selects the latter.
   const Tuning& tu = c->tune;
   // Two LDS buffers (two barriers per level, two workgroups per CU) vs one (four barriers, three per
-  // CU): with at most ~4 signals per CU the occupancy of the one-buffer kernel is not reached and the
-  // shorter per-level chain wins (measured on MI355X, db4 4096 x {512, 1024}: -3 %); VW_INV_BUF=1|2
-  // overrides.
-  bool db = !pair && (tu.inv_buf ? tu.inv_buf == 2 : B <= 4LL * c->cus);
+  // CU): with at most 2 signals per CU the occupancy of the one-buffer kernel is not reached and the
+  // shorter per-level chain wins (measured on MI355X, db4 x 4096, inverse ms one / two buffers:
+  // B = 512 0.0335 / 0.0324, B = 768 0.0462 / 0.0504, B = 1024 0.0594 / 0.0606 --
+  // profiles/r02/ab_small_batch.log, ab_inv_buf_1024_768.log); VW_INV_BUF=1|2 overrides.
+  bool db = !pair && (tu.inv_buf ? tu.inv_buf == 2 : B <= 2LL * c->cus);
   bool fused = false, fit = false;
   if (!tu.force_tiled) {
     if (pair || db) fused = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
