@@ -227,7 +227,8 @@ VW_API vw_status vw_threshold_f64(vw_ctx *ctx, double *c, int64_t B, int64_t N, 
 /* core/modwt/streaming/MODWTStreamingDenoiser.java:133-272 with core/util/MathUtils.java:94-257.
  * median_out[b] = median(|x[b][:] - center[b]|) (center NULL: median(|x[b][:]|)), exact order
  * statistics, even N = mean of the middle pair (MathUtils.median); the two passes of
- * medianAbsoluteDeviation on non-negative data.  center requires N <= 16384. */
+ * medianAbsoluteDeviation on non-negative data (any N; rows longer than 16384 with a center run the
+ * deviations through the context workspace first). */
 VW_API vw_status vw_median_f64(vw_ctx *ctx, const double *x, int64_t B, int64_t N, const double *center,
                                unsigned flags, double *median_out);
 /* out[0] = MathUtils.standardDeviation(x[0..N)) -- sequential sums, sqrt(ssd / (N-1)); N >= 2. */

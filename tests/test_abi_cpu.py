@@ -98,3 +98,21 @@ def test_wavelet_taps_match_reference_literals():
         assert abs(sum(h) - math.sqrt(2)) < 1e-6
         g = w.highPassDecomposition()
         assert g == [(1 if i % 2 == 0 else -1) * h[len(h) - 1 - i] for i in range(len(h))]
+
+
+# The reference's own tap pins: vectorwave-core/src/test/java/com/morphiqlabs/wavelet/api/
+# NewWaveletsTest.java:161-197 (value, index, tolerance exactly as asserted there).
+@pytest.mark.parametrize("name,idx,value,tol", [
+    ("DB6", 0, 0.1115407433501094, 1e-15), ("DB6", 1, 0.4946238903984530, 1e-15),
+    ("DB6", 2, 0.7511339080210954, 1e-15), ("DB6", 11, -0.0010773010853085, 1e-15),
+    ("SYM10", 0, 0.0007701598091030, 1e-15), ("SYM10", 14, 0.0057649120335782, 1e-15),
+    ("SYM10", 19, -0.0004593294205334, 1e-15),
+    ("COIF5", 0, -0.0000000960401011, 1e-15), ("COIF5", 19, 0.7742936228603274, 1e-10),
+    ("COIF5", 29, -0.0002120818620675, 1e-10),
+])
+def test_reference_tap_pins(name, idx, value, tol):
+    from vectorwave_amd.wavelets import Coiflet, Daubechies, Symlet
+    w = {"DB6": Daubechies.DB6, "SYM10": Symlet.SYM10, "COIF5": Coiflet.COIF5}[name]
+    taps = w.lowPassDecomposition()
+    assert len(taps) == {"DB6": 12, "SYM10": 20, "COIF5": 30}[name]
+    assert abs(taps[idx] - value) <= tol

@@ -39,3 +39,85 @@ def test_launcher_starts_n_ranks_with_row_blocks(n):
 def test_launcher_uneven_batch():
     out = _run("--gpus", "2", "--dry-run", "--batch", "4097")
     assert sorted((b[1], b[2]) for b in out["blocks"]) == [(0, 2049), (2049, 2048)]
+
+
+def test_no_collective_inside_timed_interval():
+    """bench.measure() on fakes that log every call: between the start of the clock (perf_counter + the
+    opening HIP event) and its end (closing event + synchronize + perf_counter) only the replay of the
+    K recorded steps runs -- the barriers of the contract lie outside."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    log = []
+
+    class Ev:
+        def __init__(self, **kw):
+            self.name = None
+
+        def record(self):
+            log.append("event")
+
+        def elapsed_time(self, other):
+            return 1.0
+
+    class FakeCuda:
+        Event = Ev
+
+        @staticmethod
+        def synchronize():
+            log.append("sync")
+
+    class FakeTorch:
+        cuda = FakeCuda
+
+    class FakeDist:
+        @staticmethod
+        def barrier():
+            log.append("barrier")
+
+    class G:
+        def launch(self, n):
+            log.append("replay")
+
+        def close(self):
+            pass
+
+    class Eng:
+        def capture(self, fn):
+            fn()
+            return G()
+
+        def reset_timing(self):
+            pass
+
+        def enable_timing(self, on):
+            pass
+
+        def kernel_time(self, k):
+            return 0.0, 0
+
+    class Wl:
+        graphs = {}
+
+        def step_fn(self, flags):
+            return lambda: log.append("step")
+
+    real = bench.time.perf_counter
+
+    def pc():
+        log.append("clock")
+        return real()
+
+    bench.time.perf_counter = pc
+    try:
+        (dev_s, host_s), _, _, _ = bench.measure(FakeTorch, FakeDist, 2, Eng(), Wl(), 0, "graph-k", 4, 1, 0.0,
+                                                 False)
+    finally:
+        bench.time.perf_counter = real
+    # the timed window: from the clock read followed by the opening event to the closing clock read
+    i0 = max(i for i in range(len(log) - 1) if log[i] == "clock" and log[i + 1] == "event")
+    i1 = max(i for i, v in enumerate(log) if v == "clock")
+    window = log[i0:i1 + 1]
+    assert window == ["clock", "event", "replay", "event", "sync", "clock"], window
+    assert "barrier" in log[:i0] and "barrier" in log[i1:]   # contract barriers, both outside
+    assert dev_s == pytest.approx(1e-3)

@@ -181,6 +181,43 @@ def test_streaming_denoiser_bit_exact(engine, est, mult, method, blk, win):
         sd.denoise(x[:blk])
 
 
+@pytest.mark.parametrize("est", ["MAD", "FIXED"])
+def test_streaming_denoiser_long_window_and_block(engine, est):
+    """MAD over a noise window / block longer than 16384 samples (the centered median's
+    register-keyed limit) -- the deviations go through the workspace, the result stays bit-exact."""
+    from vectorwave_amd import MODWTStreamingDenoiser as SD
+    from vectorwave_amd.denoise import ThresholdMethod, ThresholdType
+    w = vw.get_wavelet("db4")
+    blk, win = 20480, 20000
+    sd = (SD.builder().wavelet(w).boundaryMode(vw.BoundaryMode.PERIODIC).bufferSize(blk)
+          .thresholdType(ThresholdType.SOFT).thresholdMethod(ThresholdMethod.UNIVERSAL).thresholdMultiplier(1.5)
+          .noiseEstimation(SD.NoiseEstimation[est]).noiseWindowSize(win).build())
+    ref = O.StreamingDenoiserRestatement(w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC,
+                                         w.wavelet_id, int(ThresholdMethod.UNIVERSAL), True, 1.5, est, win)
+    x = O.java_random_signal(blk * 2, 91) + np.sin(np.arange(blk * 2) * 0.01)
+    for k in range(2):
+        blockx = x[k * blk:(k + 1) * blk]
+        np.testing.assert_array_equal(sd.denoise(blockx), ref.denoise(blockx))
+        assert sd.getEstimatedNoiseLevel() == ref.level
+    sd.close()
+
+
+def test_median_centered_long_rows(engine):
+    import torch
+    from ctypes import c_void_p
+    B, n = 3, 40001
+    v = torch.tensor(np.stack([O.java_random_signal(n, 5 + b) for b in range(B)]), device="cuda")
+    c = torch.tensor([0.1, -0.25, 0.0], dtype=torch.float64, device="cuda")
+    out = torch.empty(B, dtype=torch.float64, device="cuda")
+    engine.bind_torch_stream()
+    P = lambda t: c_void_p(t.data_ptr())  # noqa: E731
+    assert engine.lib.vw_median_f64(engine.ctx, P(v), B, n, P(c), 0, P(out)) == 0
+    torch.cuda.synchronize()
+    vh, ch = v.cpu().numpy(), c.cpu().numpy()
+    for b in range(B):
+        assert out[b].item() == O.java_median(np.abs(vh[b] - ch[b]))
+
+
 def test_streaming_denoiser_builder_validation(engine):
     from vectorwave_amd import MODWTStreamingDenoiser as SD
     for bad in (lambda b: b.bufferSize(0), lambda b: b.noiseWindowSize(-1), lambda b: b.thresholdMultiplier(0),

@@ -137,3 +137,76 @@ def test_timing_inside_captured_graph(engine):
         engine.reset_timing()
         g.close()
         assert float((y - x).abs().max()) < 1e-9
+
+
+def test_capture_of_allocating_engine_calls_keeps_storage(engine):
+    """Engine.forward inside capture() allocates its outputs; the Graph keeps them (and the
+    contiguous copy of a strided input) alive, so replays never write into storage the caching
+    allocator has handed to other tensors.  Graph.result holds fn()'s outputs, rewritten per replay."""
+    import torch
+    w = Daubechies.DB4
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        xs = torch.empty((8, 2 * 1024), dtype=torch.float64, device="cuda")
+        engine.fill_uniform(xs, 3)
+        x = xs[:, ::2]   # strided: _prep makes a contiguous copy inside the capture
+        lohi = (w.lowPassDecomposition(), w.highPassDecomposition())
+        d0, a0 = engine.forward(x, *lohi, w.wavelet_id, O.PERIODIC, 4, 0)
+        g = engine.capture(lambda: engine.forward(x, *lohi, w.wavelet_id, O.PERIODIC, 4, 0))
+        det, app = g.result
+        # churn the allocator: new tensors of the same sizes, filled with a sentinel
+        others = [torch.full_like(det, 7.0) for _ in range(4)] + [torch.full_like(app, 7.0) for _ in range(4)]
+        det.fill_(float("nan"))
+        g.launch(2)
+        torch.cuda.synchronize()
+        assert all(bool((o == 7.0).all()) for o in others), "a replay wrote into another tensor's storage"
+        assert torch.equal(det, d0) and torch.equal(app, a0)
+        g.close()
+
+
+def test_capture_exception_destroys_partial_graph(engine):
+    import torch
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        x = torch.zeros((2, 256), dtype=torch.float64, device="cuda")
+        w = Daubechies.DB4
+
+        def boom():
+            engine.forward(x, w.lowPassDecomposition(), w.highPassDecomposition(), w.wavelet_id, O.PERIODIC, 2, 0)
+            raise KeyError("inside capture")
+
+        with pytest.raises(KeyError):
+            engine.capture(boom)
+        # the context is usable again (not left capturing)
+        d, a = engine.forward(x, w.lowPassDecomposition(), w.highPassDecomposition(), w.wavelet_id, O.PERIODIC, 2, 0)
+        torch.cuda.synchronize()
+        assert bool((d == 0).all())
+
+
+def test_graph_outliving_its_context(engine):
+    """vw_ctx_destroy invalidates the context's live graphs; launching one then fails with
+    VW_ERR_STATE and destroying it is safe (no use of the freed context)."""
+    import torch
+    from ctypes import byref, c_void_p
+    lib = engine.lib
+    ctx = c_void_p()
+    assert lib.vw_ctx_create(0, byref(ctx)) == 0
+    s = torch.cuda.Stream()
+    assert lib.vw_ctx_set_stream(ctx, c_void_p(s.cuda_stream)) == 0
+    x = torch.empty((4, 512), dtype=torch.float64, device="cuda")
+    x.fill_(1.0)
+    det = torch.empty((2, 4, 512), dtype=torch.float64, device="cuda")
+    app = torch.empty((4, 512), dtype=torch.float64, device="cuda")
+    w = Daubechies.DB4
+    lo, hi = nat.taps_array(w.lowPassDecomposition()), nat.taps_array(w.highPassDecomposition())
+    P = lambda t: c_void_p(t.data_ptr())  # noqa: E731
+    torch.cuda.synchronize()
+    assert lib.vw_capture_begin(ctx) == 0
+    assert lib.vw_modwt_forward_f64(ctx, P(x), 4, 512, 512, lo, hi, 8, w.wavelet_id, 0, 2, 0, P(det), P(app)) == 0
+    g = c_void_p()
+    assert lib.vw_capture_end(ctx, byref(g)) == 0
+    assert lib.vw_graph_launch(g, 2) == 0
+    assert lib.vw_ctx_synchronize(ctx) == 0
+    assert lib.vw_ctx_destroy(ctx) == 0
+    assert lib.vw_graph_launch(g, 1) == 10   # VW_ERR_STATE
+    assert lib.vw_graph_destroy(g) == 0

@@ -2,7 +2,7 @@
 
 Bar: bit-exact in the default EXACT mode (separate multiply/add in the reference's order) for every
 index/bookkeeping path; FFT-region levels (the reference uses an FFT there) and the FMA variant
-within 1e-12 * max|x|; fp32 within 2e-5 * max|x| * J (no fp32 path exists in the reference).
+within 1e-12 * max|x|; fp32 within 1e-5 * max|x| * J (no fp32 path exists in the reference).
 """
 import math
 import os
@@ -358,7 +358,7 @@ def test_forward_persistent_matches_per_signal_kernel(engine, case):
     (d0, a0), (d1, a1) = outs
     assert torch.equal(d0, d1) and torch.equal(a0, a1)
     xh = x.double().cpu().numpy()
-    tol = 1e-12 if dt == "f64" else 2e-5 * J
+    tol = 1e-12 if dt == "f64" else 1e-5 * float(x.abs().max().item()) * J
     for b in (0, 511, 512, B - 1):
         d_ref, a_ref = O.decompose(xh[b], *lohi(w), boundary, J)
         got_d, got_a = d1[:, b, :].double().cpu().numpy(), a1[b].double().cpu().numpy()
@@ -378,7 +378,7 @@ def test_fp32_path(engine):
     det, app = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, 6, 0)
     y = engine.inverse(det, app, w.lowPassReconstruction(), w.highPassReconstruction(), w.wavelet_id, O.PERIODIC, 6,
                        nat.FLAG_CORE_LEVELS)
-    tol = 2e-5 * 6
+    tol = 1e-5 * float(np.max(np.abs(x64))) * 6
     for b in range(3):
         d, a = O.decompose(x64[b], *lohi(w), O.PERIODIC, 6, core=False)
         np.testing.assert_allclose(det[:, b, :].double().cpu().numpy(), d, rtol=0, atol=tol)

@@ -13,6 +13,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <set>
 #include <string>
 #include <vector>
 
@@ -136,6 +137,8 @@ static Tuning read_tuning() {
   return t;
 }
 
+struct vw_graph;
+
 struct vw_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -155,7 +158,27 @@ struct vw_ctx {
   std::vector<TimedLaunch> captured;   // timed launches recorded during the current capture
   std::vector<hipEvent_t> event_pool;
   std::map<std::string, std::pair<double, int64_t>> totals;
+  std::set<vw_graph*> graphs;          // live graphs recorded on this context (invalidated at destroy)
 };
+
+struct vw_graph {
+  vw_ctx* ctx = nullptr;          // nullptr once the context is destroyed (the graph is then dead)
+  int device = 0;
+  unsigned ws_gen = 0;
+  std::vector<TimedLaunch> timed;  // event-record nodes (timing enabled at capture)
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+};
+
+// Frees the HIP objects of a graph (its context's device must be current).
+static void release_graph(vw_graph* gr) {
+  for (auto& t : gr->timed) { hipEventDestroy(t.start); hipEventDestroy(t.stop); }
+  gr->timed.clear();
+  if (gr->exec) hipGraphExecDestroy(gr->exec);
+  if (gr->graph) hipGraphDestroy(gr->graph);
+  gr->exec = nullptr;
+  gr->graph = nullptr;
+}
 
 struct vw_stream {
   vw_ctx* ctx = nullptr;
@@ -399,8 +422,23 @@ extern "C" vw_status vw_ctx_create(int device, vw_ctx** out) {
 extern "C" vw_status vw_ctx_destroy(vw_ctx* c) {
   if (!c) return fail(VW_ERR_NULL, "ctx is null");
   hipSetDevice(c->device);
+  if (c->capturing) {  // an unfinished capture: end it and drop what it recorded
+    hipGraph_t gph = nullptr;
+    if (hipStreamEndCapture(c->stream, &gph) == hipSuccess && gph) hipGraphDestroy(gph);
+    (void)hipGetLastError();
+    for (auto& t : c->captured) { hipEventDestroy(t.start); hipEventDestroy(t.stop); }
+    c->captured.clear();
+    c->capturing = false;
+  }
   hipStreamSynchronize(c->stream);
   collect_timing(c);
+  // graphs outliving their context: free their HIP objects now; the handles stay valid for
+  // vw_graph_destroy, and vw_graph_launch on them fails with VW_ERR_STATE
+  for (vw_graph* gr : c->graphs) {
+    release_graph(gr);
+    gr->ctx = nullptr;
+  }
+  c->graphs.clear();
   for (auto e : c->event_pool) hipEventDestroy(e);
   if (c->ws) hipFree(c->ws);
   if (c->ws2) hipFree(c->ws2);
@@ -464,13 +502,6 @@ extern "C" vw_status vw_ctx_set_stream(vw_ctx* c, void* s) {
 // one host call -- the host-side planning, argument packing and per-kernel launch cost of the
 // transforms are paid once at capture.  Calls that must synchronize (validation, host memory,
 // SYNC, workspace growth) are rejected while capturing.
-struct vw_graph {
-  vw_ctx* ctx = nullptr;
-  unsigned ws_gen = 0;
-  std::vector<TimedLaunch> timed;  // event-record nodes (timing enabled at capture)
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
-};
 
 extern "C" vw_status vw_capture_begin(vw_ctx* c) {
   if (!c) return fail(VW_ERR_NULL, "ctx is null");
@@ -509,37 +540,51 @@ extern "C" vw_status vw_capture_end(vw_ctx* c, vw_graph** out) {
   vw_graph* gr = new vw_graph();
   gr->timed.swap(timed);
   gr->ctx = c;
+  gr->device = c->device;
   gr->ws_gen = c->ws_gen;
   gr->graph = graph;
   gr->exec = exec;
+  c->graphs.insert(gr);
   *out = gr;
   return ok();
 }
 
+
 extern "C" vw_status vw_graph_launch(vw_graph* gr, int64_t count) {
   if (!gr) return fail(VW_ERR_NULL, "graph is null");
   vw_ctx* c = gr->ctx;
+  if (!c) return fail(VW_ERR_STATE, "the context of this graph was destroyed");
   std::lock_guard<std::recursive_mutex> g(c->mu);
   if (gr->ws_gen != c->ws_gen)
     return fail(VW_ERR_STATE, "the context workspace moved since this graph was recorded; record it again");
   hipSetDevice(c->device);
   for (int64_t i = 0; i < count; ++i) VW_HIP(hipGraphLaunch(gr->exec, c->stream));
-  // timed launches recorded inside the graph: their events hold the LAST replay of this call
-  if (c->timing && count > 0)
+  // Timed launches recorded inside the graph: their events hold the LAST replay only, so a graph's
+  // entries are pending at most once (a second launch before a collect replaces, not duplicates, them).
+  if (c->timing && count > 0 && !gr->timed.empty()) {
+    std::set<hipEvent_t> mine;
+    for (const auto& t : gr->timed) mine.insert(t.start);
+    c->pending.erase(std::remove_if(c->pending.begin(), c->pending.end(),
+                                    [&](const TimedLaunch& t) { return t.graph_owned && mine.count(t.start); }),
+                     c->pending.end());
     for (const auto& t : gr->timed) c->pending.push_back(t);
+  }
   return ok();
 }
 
 extern "C" vw_status vw_graph_destroy(vw_graph* gr) {
   if (!gr) return fail(VW_ERR_NULL, "graph is null");
   vw_ctx* c = gr->ctx;
+  if (!c) {  // context already destroyed: it released the HIP objects
+    delete gr;
+    return ok();
+  }
   std::lock_guard<std::recursive_mutex> g(c->mu);
   hipSetDevice(c->device);
   hipStreamSynchronize(c->stream);
   collect_timing(c);  // pending entries may reference this graph's events
-  for (auto& t : gr->timed) { hipEventDestroy(t.start); hipEventDestroy(t.stop); }
-  if (gr->exec) hipGraphExecDestroy(gr->exec);
-  if (gr->graph) hipGraphDestroy(gr->graph);
+  release_graph(gr);
+  c->graphs.erase(gr);
   delete gr;
   return ok();
 }
@@ -1090,7 +1135,10 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   // shorter per-level chain wins (measured on MI355X, db4 x 4096, inverse ms one / two buffers:
   // B = 512 0.0335 / 0.0324, B = 768 0.0462 / 0.0504, B = 1024 0.0594 / 0.0606 --
   // profiles/r02/ab_small_batch.log, ab_inv_buf_1024_768.log); VW_INV_BUF=1|2 overrides.
-  bool db = !pair && (tu.inv_buf ? tu.inv_buf == 2 : B <= 2LL * c->cus);
+  // Long PERIODIC filters (L >= VW_BLK) keep the register-blocked single-buffer kernel (k_inverse_blk
+  // needs !db) at small batches too: its NV+L-1 LDS reads per branch outweigh the shorter barrier chain.
+  const bool blk_pref = tu.blk > 0 && L >= tu.blk && boundary == VW_PERIODIC;
+  bool db = !pair && (tu.inv_buf ? tu.inv_buf == 2 : (B <= 2LL * c->cus && !blk_pref));
   bool fused = false, fit = false;
   if (!tu.force_tiled) {
     if (pair || db) fused = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
@@ -1735,11 +1783,22 @@ extern "C" vw_status vw_median_f64(vw_ctx* c, const double* x, int64_t B, int64_
                                    unsigned flags, double* median_out) {
   if (!c || !x || !median_out) return fail(VW_ERR_NULL, "null argument");
   if (B <= 0 || N <= 0) return fail(VW_ERR_EMPTY, "Array cannot be null or empty");
-  if (center && N > 16384) return fail(VW_ERR_UNSUPPORTED, "centered median supports N <= 16384");
+  if (N > (1LL << 30)) return fail(VW_ERR_ARG, "row too long");
   if (flags & VW_FLAG_HOST_MEMORY) return fail(VW_ERR_UNSUPPORTED, "device pointers only");
   std::lock_guard<std::recursive_mutex> g(c->mu);
   hipSetDevice(c->device);
-  hipError_t e = launch_median(x, N, B, (int)N, center, median_out, c->stream);
+  hipError_t e;
+  if (center && N > kSigmaRegN) {
+    // rows beyond the register-keyed centered path: deviations |x - center| into the workspace, then
+    // the uncentered selection (any N) on them -- the same keys, the same exact order statistic
+    if (B > 65535) return fail(VW_ERR_UNSUPPORTED, "centered median of more than 65535 long rows");
+    VW_TRY(ensure_ws(c, (size_t)B * (size_t)N * sizeof(double)));
+    double* dev = reinterpret_cast<double*>(c->ws);
+    e = launch_abs_center(x, N, B, (int)N, center, dev, c->stream);
+    if (e == hipSuccess) e = launch_median(dev, N, B, (int)N, nullptr, median_out, c->stream);
+  } else {
+    e = launch_median(x, N, B, (int)N, center, median_out, c->stream);
+  }
   if (e != hipSuccess) return fail(VW_ERR_DEVICE, "launch failed: %s", hipGetErrorString(e));
   if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
   return ok();

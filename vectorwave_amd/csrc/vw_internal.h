@@ -171,6 +171,7 @@ struct MultiArgs {
 // WaveletDenoiser threshold methods (core/denoising/WaveletDenoiser.java:588-622) and the per-launch
 // constants of the threshold kernels (vw_sigma.h).
 enum ThrMethod { kThrUniversal = 0, kThrSure = 1, kThrMinimax = 2, kThrBayes = 3, kThrFixed = 4 };
+constexpr int kSigmaRegN = 16384;  // k_noise_sigma keeps a row's keys in registers up to this N (1024 x 16)
 constexpr int kSureMaxN = 16384;  // SURE on device: the sorted row lives in LDS
 struct DenoiseConsts {
   double level_scale[kMaxLevels];  // Math.sqrt(1 << level) (denoiseMultiLevel, :225), 1 for denoise()
@@ -212,6 +213,10 @@ hipError_t launch_noise_sigma(const double* coeffs, long long ld, long long B, i
 // Exact median of |x - center| per row (center nullptr: of |x|); N <= 16384 when center is given.
 hipError_t launch_median(const double* x, long long ld, long long B, int N, const double* center, double* median_out,
                          hipStream_t st);
+// out[b][i] = |x[b*ld + i] - center[b]| (MathUtils.medianAbsoluteDeviation's deviations), for the
+// centered median of rows longer than the register-keyed path holds.
+hipError_t launch_abs_center(const double* x, long long ld, long long B, int N, const double* center, double* out,
+                             hipStream_t st);
 hipError_t launch_seq_std(const double* x, int n, double* out, hipStream_t st);
 hipError_t launch_gather_abs(const double* src, const int* idx, int count, double* window, int wsize, int start,
                              hipStream_t st);

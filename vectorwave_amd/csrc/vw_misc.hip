@@ -60,6 +60,22 @@ hipError_t launch_median(const double* x, long long ld, long long B, int N, cons
   return hipGetLastError();
 }
 
+__global__ void __launch_bounds__(256) k_abs_center(const double* __restrict__ x, long long ld, int N,
+                                                    const double* __restrict__ center, double* __restrict__ out) {
+  const long long b = blockIdx.y;
+  const double c = center[b];
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N; i += gridDim.x * blockDim.x)
+    out[b * (long long)N + i] = __builtin_fabs(x[b * ld + i] - c);  // Math.abs(values[i] - median)
+}
+
+hipError_t launch_abs_center(const double* x, long long ld, long long B, int N, const double* center, double* out,
+                             hipStream_t st) {
+  if (B > 65535) return hipErrorInvalidConfiguration;
+  const unsigned gx = (unsigned)std::min(std::max((N + 255) / 256, 1), 1024);
+  hipLaunchKernelGGL(k_abs_center, dim3(gx, (unsigned)B), dim3(256), 0, st, x, ld, N, center, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_seq_std(const double* x, int n, double* out, hipStream_t st) {
   hipLaunchKernelGGL(k_seq_std, dim3(1), dim3(64), 0, st, x, n, out);
   return hipGetLastError();

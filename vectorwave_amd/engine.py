@@ -46,6 +46,7 @@ class Engine:
         _check(self.lib.vw_ctx_create(device, byref(ctx)))
         self.ctx = ctx
         self._ext_stream = None
+        self._keep = None   # during capture(): device tensors the recorded calls allocate or convert
 
     @classmethod
     def get(cls, device: Optional[int] = None) -> "Engine":
@@ -120,6 +121,8 @@ class Engine:
             if x.device.index != self.device:
                 raise ValueError(f"tensor on cuda:{x.device.index}, engine on cuda:{self.device}")
             self.bind_torch_stream()
+            if self._keep is not None:
+                self._keep.append(x)   # a recorded graph reads this storage on every replay
             return x, True, c_void_p(x.data_ptr()), x.dtype == torch.float32
         if torch is not None and isinstance(x, torch.Tensor):
             x = x.detach().numpy()
@@ -131,7 +134,10 @@ class Engine:
 
     def _empty(self, like, is_dev, shape):
         if is_dev:
-            return torch.empty(shape, dtype=like.dtype, device=like.device)
+            t = torch.empty(shape, dtype=like.dtype, device=like.device)
+            if self._keep is not None:
+                self._keep.append(t)   # a recorded graph writes this storage on every replay
+            return t
         return np.empty(shape, dtype=like.dtype)
 
     @staticmethod
@@ -259,16 +265,28 @@ class Engine:
     # -- captured steps (vw_capture_begin / vw_capture_end / vw_graph_launch) --------------------
     def capture(self, fn) -> "Graph":
         """Record the engine calls ``fn()`` makes (device tensors, no validation) into one HIP graph.
-        The engine must be bound to a non-default torch stream (``bind_torch_stream``)."""
+        The engine must be bound to a non-default torch stream (``bind_torch_stream``).
+
+        Every device tensor the recorded calls allocate (outputs) or convert (inputs made contiguous /
+        cast) is kept alive by the returned Graph, so the caching allocator never hands that storage to
+        another tensor while replays still write it; ``Graph.result`` is ``fn()``'s return value, whose
+        tensors every replay rewrites.  If ``fn()`` raises, the partial graph is destroyed."""
         self.bind_torch_stream()
         _check(self.lib.vw_capture_begin(self.ctx))
+        self._keep = []
+        done = False
+        result = None
         try:
-            fn()
+            result = fn()
+            done = True
         finally:
+            keep, self._keep = self._keep, None
             g = c_void_p()
             st = self.lib.vw_capture_end(self.ctx, byref(g))
+            if not done and st == 0:
+                self.lib.vw_graph_destroy(g)
         _check(st)
-        return Graph(self, g)
+        return Graph(self, g, keep=keep, result=result)
 
     def fill_uniform(self, x, seed: int, offset: int = 0):
         """Device generator of the bench input: x = 2u-1, u = (splitmix64(seed ^ (offset+i)) >> 11) 2^-53."""
@@ -283,9 +301,11 @@ class Engine:
 class Graph:
     """An executable HIP graph of recorded engine calls; ``launch(count)`` replays it on the stream."""
 
-    def __init__(self, engine: Engine, handle: c_void_p):
+    def __init__(self, engine: Engine, handle: c_void_p, keep=None, result=None):
         self.engine = engine
         self.handle = handle
+        self._keep = keep or []   # storage the recorded kernels read / write (see Engine.capture)
+        self.result = result
 
     def launch(self, count: int = 1) -> None:
         _check(self.engine.lib.vw_graph_launch(self.handle, int(count)))
@@ -294,6 +314,7 @@ class Graph:
         if self.handle:
             _check(self.engine.lib.vw_graph_destroy(self.handle))
             self.handle = None
+        self._keep = []
 
     def __del__(self):  # pragma: no cover
         try:
