@@ -2,14 +2,15 @@
 # PMC passes over a short bench run (one counter group per rocprofv3 invocation; no tracing domains).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out/pmc
+PMC_DIR="${PMC_DIR:-gpurun_out/pmc}"
+mkdir -p "$PMC_DIR"
 export TMPDIR=/tmp
 ARGS="${BENCH_ARGS:-} --no-cpu-baseline --no-alt --steps 3 --warmup 1"
 i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d gpurun_out/pmc/p$i -o pmc -- python3 bench.py $ARGS > gpurun_out/pmc/p$i.log 2>&1; rc=$?
+  timeout -k 10 240 rocprofv3 --pmc $grp --output-format csv -d "$PMC_DIR/p$i" -o pmc -- python3 bench.py $ARGS > "$PMC_DIR/p$i.log" 2>&1; rc=$?
   echo "group $i ($grp) rc=$rc"
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then exit $rc; fi
 done <<< "${PMC_GROUPS:-FETCH_SIZE
