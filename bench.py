@@ -84,6 +84,11 @@ def parse(argv=None):
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--dry-run", action="store_true",
                    help="CPU only: launch the ranks, shard, run the timing collectives (gloo), print the plan")
+    p.add_argument("--ref-shapes", action="store_true",
+                   help="the reference's own JMH shapes (MultiLevelBatchSIMDBenchmark) through the host-memory "
+                        "(JNI-shaped) path: per-call us with H2D / kernel / D2H separated, beside the CPU "
+                        "restatement on the same rows; one JSON line (and --out FILE)")
+    p.add_argument("--out", default="", help="--ref-shapes: also write the JSON to this file")
     return p.parse_args(argv)
 
 
@@ -128,7 +133,117 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.dry_run:
         return dry_run(args, world, rank)
+    if args.ref_shapes:
+        return ref_shapes(args)
     run(args, world, rank, local)
+
+
+# ---------------------------------------------------------------------------------------------
+# The reference's measurement shapes (vectorwave-benchmarks/src/main/java/com/morphiqlabs/benchmark/
+# MultiLevelBatchSIMDBenchmark.java:29-36): batch {8,16,32} x N {4096,8192} x {db4, haar} x J {3,5},
+# multi-level forward, PERIODIC.  This is the regime of a BatchMODWT / MultiLevelMODWTTransform caller:
+# small batches handed over as host arrays, where staging and launch latency dominate.
+REF_SHAPES = [(B, n, wv, J) for B in (8, 16, 32) for n in (4096, 8192) for wv in ("db4", "haar") for J in (3, 5)]
+
+
+def ref_shapes(args):
+    import statistics
+
+    import numpy as np
+    import torch
+
+    import vectorwave_amd as vw
+    from vectorwave_amd import _native as nat
+
+    eng = vw.Engine.get(0)
+    lib = eng.lib
+    reps = 30
+    rows = []
+    P = lambda a: c_void_p(a.ctypes.data)  # noqa: E731
+    D = lambda t: c_void_p(t.data_ptr())   # noqa: E731
+
+    def med_us(fn, n=reps):
+        fn()
+        ts = []
+        for _ in range(n):
+            t0 = time.perf_counter()
+            fn()
+            ts.append(time.perf_counter() - t0)
+        return statistics.median(ts) * 1e6
+
+    for B, n, wname, J in REF_SHAPES:
+        w = vw.get_wavelet(wname)
+        lo, hi = nat.taps_array(w.lowPassDecomposition()), nat.taps_array(w.highPassDecomposition())
+        L = len(w.lowPassDecomposition())
+        J = min(J, vw.max_levels(n, L))   # the benchmark's own clamp (getMaximumLevels)
+        rng = np.random.default_rng(42)
+        x = rng.standard_normal((B, n))   # nextGaussian-shaped input
+        det = np.empty((J, B, n))
+        app = np.empty((B, n))
+        fl_host = nat.FLAG_HOST_MEMORY | nat.FLAG_CORE_LEVELS
+
+        def host_call():
+            st = lib.vw_modwt_forward_f64(eng.ctx, P(x), B, n, n, lo, hi, L, w.wavelet_id, nat.PERIODIC, J, fl_host,
+                                          P(det), P(app))
+            if st:
+                raise RuntimeError(nat.last_error())
+        call_us = med_us(host_call)
+        # the same call's parts: H2D of x, the device-resident forward, D2H of the J + 1 output planes
+        xd = torch.empty((B, n), dtype=torch.float64, device="cuda")
+        dd = torch.empty((J, B, n), dtype=torch.float64, device="cuda")
+        ad = torch.empty((B, n), dtype=torch.float64, device="cuda")
+        eng.bind_torch_stream()
+        h2d_us = med_us(lambda: lib.vw_memcpy(eng.ctx, D(xd), P(x), x.nbytes, 0))
+        d2h_us = med_us(lambda: (lib.vw_memcpy(eng.ctx, P(det), D(dd), det.nbytes, 1),
+                                 lib.vw_memcpy(eng.ctx, P(app), D(ad), app.nbytes, 1)))
+        lib.vw_memcpy(eng.ctx, D(xd), P(x), x.nbytes, 0)
+
+        def dev_call():
+            lib.vw_modwt_forward_f64(eng.ctx, D(xd), B, n, n, lo, hi, L, w.wavelet_id, nat.PERIODIC, J,
+                                     nat.FLAG_CORE_LEVELS, D(dd), D(ad))
+        dev_call()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            dev_call()
+        e1.record()
+        torch.cuda.synchronize()
+        kernel_us = e0.elapsed_time(e1) * 1e3 / reps
+        host_call()   # det / app again from the host-memory call (the D2H timing copied other bytes there)
+        cpu_us, same = ref_shapes_cpu(x, w, J, det, app)
+        rows.append({"batch": B, "n": n, "wavelet": wname, "levels": J, "gpu_host_call_us": round(call_us, 1),
+                     "h2d_us": round(h2d_us, 1), "device_forward_us": round(kernel_us, 2), "d2h_us": round(d2h_us, 1),
+                     "h2d_GBps": round(x.nbytes / h2d_us / 1e3, 2),
+                     "d2h_GBps": round((det.nbytes + app.nbytes) / d2h_us / 1e3, 2),
+                     "cpu_scalar_us": round(cpu_us, 1), "cpu_over_gpu_call": round(cpu_us / call_us, 2),
+                     "bit_exact_vs_restatement": same})
+    out = {"mode": "ref-shapes", "source": "MultiLevelBatchSIMDBenchmark.java:29-36 (multi-level forward, PERIODIC)",
+           "gpu_path": "vw_modwt_forward_f64 with VW_FLAG_HOST_MEMORY from pageable numpy arrays (the JNI shape): "
+                       "H2D, fused forward kernel, D2H, synchronize; median of %d calls" % reps,
+           "cpu_path": "C restatement of MultiLevelMODWTTransform.decompose per signal (zero taps included), "
+                       "1 thread, as the JMH scalar_multiLevel benchmark (Scope.Thread)",
+           "shapes": rows}
+    line = json.dumps(out)
+    if args.out:
+        with open(args.out, "w") as fh:
+            fh.write(line + "\n")
+    print(line, flush=True)
+
+
+def ref_shapes_cpu(x, w, J, det, app):
+    """CPU leg of --ref-shapes (the checker / baseline, outside any GPU timing): the restatement of
+    vectorwave-core's decompose per signal on one thread; also checks the GPU rows bit for bit."""
+    import numpy as np
+    from oracle import oracle as O
+
+    lo, hi = w.lowPassDecomposition(), w.highPassDecomposition()
+    same = True
+    t0 = time.perf_counter()
+    for b in range(x.shape[0]):
+        d, a = O.decompose(x[b], lo, hi, O.PERIODIC, J)   # single-threaded at these N (vw_oracle.c)
+        same = same and bool(np.array_equal(d, det[:, b, :]) and np.array_equal(a, app[b]))
+    return (time.perf_counter() - t0) * 1e6, same
 
 
 def dry_run(args, world, rank):

@@ -47,9 +47,11 @@
  * [J][B][N] (level 1 = finest first; BatchMODWT's detailPerLevel order),
  * approx [B][N], y [B][N].
  *
- * Threading: one vw_ctx per device; a context may be used from several host
- * threads, calls are serialized on its stream.  The engine retains no caller
- * buffer after a call returns.
+ * Threading: a context may be used from several host threads (calls are
+ * serialized by its mutex and run on its stream); several contexts -- on one
+ * device or on several -- run concurrently from different threads, e.g. through
+ * vw_modwt_forward_multi_f64.  The engine retains no caller buffer after a
+ * call returns (host-memory calls stage through a pool the context keeps).
  */
 #ifndef VECTORWAVE_AMD_H
 #define VECTORWAVE_AMD_H
@@ -171,6 +173,24 @@ VW_API vw_status vw_modwt_inverse_f32(vw_ctx *ctx, const float *details, const f
                                       int64_t B, int64_t N, const double *lo, const double *hi, int L,
                                       int wavelet_id, int boundary, int J, unsigned detail_mask,
                                       int approx_zero, unsigned flags, float *y);
+
+/* ---- one batch over several contexts (one host thread per context) ----------------------------
+ * Replaces the reference's in-process parallelism over one batch call: BatchMODWT.multiLevelAoS /
+ * inverseMultiLevelAoS (ext/extensions/modwt/BatchMODWT.java:90-111, :151-178) and the
+ * VectorWaveSwtAdapter executor (core/swt/VectorWaveSwtAdapter.java:210-267).  The B rows are split
+ * into n contiguous blocks (the first B % n blocks one row longer; min(n, B) blocks), block k runs on
+ * ctxs[k] from its own host thread (ctxs[0] on the calling thread); the call returns when every
+ * block is done.  Contexts may live on different devices or share one.  flags must include
+ * VW_FLAG_HOST_MEMORY: the arrays are the caller's host arrays, laid out as the single-context
+ * calls (details [J][B][N]); each thread stages its block through its context.  Errors: the first
+ * failing block's status; vw_last_error() names the block. */
+VW_API vw_status vw_modwt_forward_multi_f64(vw_ctx *const *ctxs, int nctx, const double *x, int64_t B, int64_t N,
+                                            int64_t ldx, const double *lo, const double *hi, int L, int wavelet_id,
+                                            int boundary, int J, unsigned flags, double *details, double *approx);
+VW_API vw_status vw_modwt_inverse_multi_f64(vw_ctx *const *ctxs, int nctx, const double *details,
+                                            const double *approx, int64_t B, int64_t N, const double *lo,
+                                            const double *hi, int L, int wavelet_id, int boundary, int J,
+                                            unsigned detail_mask, int approx_zero, unsigned flags, double *y);
 
 /* ---- single-level MODWT (MODWTTransform: pairwise inverse sums, any N >= 1) --- */
 VW_API vw_status vw_modwt1_forward_f64(vw_ctx *ctx, const double *x, int64_t B, int64_t N, int64_t ldx,

@@ -22,6 +22,7 @@ from .streaming import (MODWTStreamingDenoiser, MODWTStreamingTransform, MODWTSt
                         MultiLevelMODWTStreamingTransform)
 from .batch import BatchMODWT, BatchSIMDMODWT, BatchStreamingMODWT
 from .engine import Engine, max_levels, version
+from .multidevice import DeviceGroup
 
 __all__ = [
     "Coiflet", "Daubechies", "Haar", "Symlet", "Wavelet", "available_wavelets", "get_wavelet",
@@ -30,5 +31,5 @@ __all__ = [
     "MultiLevelMODWTTransform", "MutableMultiLevelMODWTResult", "VectorWaveSwtAdapter", "BatchMODWT",
     "WaveletDenoiser", "ThresholdMethod", "ThresholdType", "BatchSIMDMODWT", "MODWTStreamingTransform",
     "MODWTStreamingTransformImpl", "MultiLevelMODWTStreamingTransform",
-    "BatchStreamingMODWT", "Engine", "max_levels", "version",
+    "BatchStreamingMODWT", "Engine", "max_levels", "version", "DeviceGroup",
 ]

@@ -50,6 +50,11 @@ SIGNATURES = {
                                      c_int, c_uint, c_int, c_uint, c_void_p]),
     "vw_modwt_inverse_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, _dp, _dp, c_int, c_int, c_int,
                                      c_int, c_uint, c_int, c_uint, c_void_p]),
+    # ctxs: a (c_void_p * n) array of vw_ctx handles
+    "vw_modwt_forward_multi_f64": (c_int, [c_void_p, c_int, c_void_p, c_int64, c_int64, c_int64, _dp, _dp, c_int,
+                                           c_int, c_int, c_int, c_uint, c_void_p, c_void_p]),
+    "vw_modwt_inverse_multi_f64": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int64, _dp, _dp, c_int,
+                                           c_int, c_int, c_int, c_uint, c_int, c_uint, c_void_p]),
     "vw_modwt1_forward_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, _dp, _dp, c_int, c_int, c_uint,
                                       c_void_p, c_void_p]),
     "vw_modwt1_inverse_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, _dp, _dp, c_int, c_int, c_uint,

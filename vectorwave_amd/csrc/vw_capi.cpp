@@ -15,6 +15,7 @@
 #include <mutex>
 #include <set>
 #include <string>
+#include <thread>
 #include <vector>
 
 using namespace vw;
@@ -159,6 +160,7 @@ struct vw_ctx {
   std::vector<hipEvent_t> event_pool;
   std::map<std::string, std::pair<double, int64_t>> totals;
   std::set<vw_graph*> graphs;          // live graphs recorded on this context (invalidated at destroy)
+  std::vector<std::pair<void*, size_t>> stage;  // host-memory staging pool (Staging), kept across calls
 };
 
 struct vw_graph {
@@ -442,6 +444,7 @@ extern "C" vw_status vw_ctx_destroy(vw_ctx* c) {
   for (auto e : c->event_pool) hipEventDestroy(e);
   if (c->ws) hipFree(c->ws);
   if (c->ws2) hipFree(c->ws2);
+  for (auto& b : c->stage) hipFree(b.first);
   if (c->bad) hipFree(c->bad);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
@@ -1325,21 +1328,53 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
 }
 
 // ------------------------------------------------------------------------------------------------
-// Host-memory staging (the JNI / FFM path): copy in, run on device, copy out, synchronize.
+// Host-memory staging (the JNI / FFM path): copy in, run on device, copy out, synchronize.  Device
+// buffers are carved from the context's staging pool (blocks kept across calls, never hipMalloc /
+// hipFree per call: a JNI caller's per-batch loop pays only the copies and the kernels).  A call
+// carves from offset 0 of the pool; its destructor synchronizes the stream, so the next call may
+// reuse the same bytes.  Calls on one context are serialized by its mutex.
 struct Staging {
   vw_ctx* c;
-  std::vector<std::pair<void*, size_t>> allocs;
+  size_t used_block = 0, used_off = 0;
   explicit Staging(vw_ctx* ctx) : c(ctx) {}
-  ~Staging() {
-    hipStreamSynchronize(c->stream);
-    for (auto& a : allocs) hipFree(a.first);
+  ~Staging() { hipStreamSynchronize(c->stream); }
+  vw_status carve(size_t bytes, void** out) {
+    bytes = align_up(std::max<size_t>(bytes, 16), 256);
+    for (; used_block < c->stage.size(); ++used_block, used_off = 0) {
+      auto& blk = c->stage[used_block];
+      if (used_off + bytes <= blk.second) {
+        *out = static_cast<char*>(blk.first) + used_off;
+        used_off += bytes;
+        return VW_OK;
+      }
+    }
+    const size_t last = c->stage.empty() ? 0 : c->stage.back().second;
+    const size_t want = std::max({bytes, 2 * last, (size_t)4 << 20});
+    void* p = nullptr;
+    VW_HIP(hipMalloc(&p, want));
+    c->stage.push_back({p, want});
+    used_block = c->stage.size() - 1;
+    used_off = bytes;
+    *out = p;
+    return VW_OK;
   }
   template <typename T>
   vw_status in(const T* host, size_t count, T** dev) {
     void* p = nullptr;
-    VW_HIP(hipMalloc(&p, std::max<size_t>(count * sizeof(T), 16)));
-    allocs.push_back({p, count});
+    VW_TRY(carve(count * sizeof(T), &p));
     if (host && count) VW_HIP(hipMemcpyAsync(p, host, count * sizeof(T), hipMemcpyHostToDevice, c->stream));
+    *dev = reinterpret_cast<T*>(p);
+    return VW_OK;
+  }
+  // `planes` blocks of `count` elements, the host blocks `host_stride` elements apart (a row block of a
+  // [planes][B][N] host array), packed on the device
+  template <typename T>
+  vw_status in_planes(const T* host, size_t planes, size_t count, size_t host_stride, T** dev) {
+    void* p = nullptr;
+    VW_TRY(carve(planes * count * sizeof(T), &p));
+    if (host && count && planes)
+      VW_HIP(hipMemcpy2DAsync(p, count * sizeof(T), host, host_stride * sizeof(T), count * sizeof(T), planes,
+                              hipMemcpyHostToDevice, c->stream));
     *dev = reinterpret_cast<T*>(p);
     return VW_OK;
   }
@@ -1348,8 +1383,51 @@ struct Staging {
     if (host && count) VW_HIP(hipMemcpyAsync(host, dev, count * sizeof(T), hipMemcpyDeviceToHost, c->stream));
     return VW_OK;
   }
+  template <typename T>
+  vw_status out_planes(T* host, const T* dev, size_t planes, size_t count, size_t host_stride) {
+    if (host && count && planes)
+      VW_HIP(hipMemcpy2DAsync(host, host_stride * sizeof(T), dev, count * sizeof(T), count * sizeof(T), planes,
+                              hipMemcpyDeviceToHost, c->stream));
+    return VW_OK;
+  }
 };
 
+
+// Host-memory forward of B rows: x[B][ldx] in, details as J host planes `det_stride` elements apart
+// (B * N for a whole batch; the global B * N for a row block of a sharded batch), approx [B][N].
+// Caller holds c->mu.  Synchronous.
+template <typename T>
+static vw_status forward_host(vw_ctx* c, const T* x, int64_t B, int64_t N, int64_t ldx, const double* lo,
+                              const double* hi, int L, int boundary, int J, unsigned flags, T* details,
+                              int64_t det_stride, T* approx) {
+  Staging s(c);
+  T *dx, *dd, *da;
+  VW_TRY(s.in(x, (size_t)(B - 1) * ldx + N, &dx));  // (the last row's padding need not exist)
+  VW_TRY(s.in<T>(nullptr, (size_t)J * B * N, &dd));
+  VW_TRY(s.in<T>(nullptr, (size_t)B * N, &da));
+  VW_TRY(forward_impl<T>(c, dx, B, N, ldx, lo, hi, L, boundary, J, flags & ~(VW_FLAG_SYNC | VW_FLAG_HOST_MEMORY), dd,
+                         da, false, -1, nullptr, false));
+  VW_TRY(s.out_planes(details, dd, (size_t)J, (size_t)(B * N), (size_t)det_stride));
+  VW_TRY(s.out(approx, da, (size_t)B * N));
+  VW_HIP(hipStreamSynchronize(c->stream));
+  return VW_OK;
+}
+
+template <typename T>
+static vw_status inverse_host(vw_ctx* c, const T* details, int64_t det_stride, const T* approx, int64_t B, int64_t N,
+                              const double* lo, const double* hi, int L, int wid, int boundary, int J,
+                              unsigned detail_mask, int approx_zero, unsigned flags, T* y) {
+  Staging s(c);
+  T *dd = nullptr, *da = nullptr, *dy;
+  if (detail_mask) VW_TRY(s.in_planes(details, (size_t)J, (size_t)(B * N), (size_t)det_stride, &dd));
+  if (!approx_zero) VW_TRY(s.in(approx, (size_t)B * N, &da));
+  VW_TRY(s.in<T>(nullptr, (size_t)B * N, &dy));
+  VW_TRY(inverse_impl<T>(c, dd, da, B, N, lo, hi, L, wid, boundary, J, detail_mask, approx_zero,
+                         flags & ~(VW_FLAG_SYNC | VW_FLAG_HOST_MEMORY), dy, false, nullptr, 0));
+  VW_TRY(s.out(y, dy, (size_t)B * N));
+  VW_HIP(hipStreamSynchronize(c->stream));
+  return VW_OK;
+}
 
 template <typename T>
 static vw_status modwt_forward(vw_ctx* c, const T* x, int64_t B, int64_t N, int64_t ldx, const double* lo,
@@ -1363,16 +1441,7 @@ static vw_status modwt_forward(vw_ctx* c, const T* x, int64_t B, int64_t N, int6
   std::lock_guard<std::recursive_mutex> g(c->mu);
   hipSetDevice(c->device);
   if (flags & VW_FLAG_HOST_MEMORY) {
-    Staging s(c);
-    T *dx, *dd, *da;
-    VW_TRY(s.in(x, (size_t)B * ldx, &dx));
-    VW_TRY(s.in<T>(nullptr, (size_t)J * B * N, &dd));
-    VW_TRY(s.in<T>(nullptr, (size_t)B * N, &da));
-    VW_TRY(forward_impl<T>(c, dx, B, N, ldx, lo, hi, L, boundary, J, flags & ~VW_FLAG_SYNC, dd, da, false, -1,
-                           nullptr, false));
-    VW_TRY(s.out(details, dd, (size_t)J * B * N));
-    VW_TRY(s.out(approx, da, (size_t)B * N));
-    VW_HIP(hipStreamSynchronize(c->stream));
+    VW_TRY(forward_host<T>(c, x, B, N, ldx, lo, hi, L, boundary, J, flags, details, B * N, approx));
     return ok();
   }
   VW_TRY(forward_impl<T>(c, x, B, N, ldx, lo, hi, L, boundary, J, flags, details, approx, false, -1, nullptr, false));
@@ -1396,15 +1465,8 @@ static vw_status modwt_inverse(vw_ctx* c, const T* details, const T* approx, int
   std::lock_guard<std::recursive_mutex> g(c->mu);
   hipSetDevice(c->device);
   if (flags & VW_FLAG_HOST_MEMORY) {
-    Staging s(c);
-    T *dd = nullptr, *da = nullptr, *dy;
-    if (detail_mask) VW_TRY(s.in(details, (size_t)J * B * N, &dd));
-    if (!approx_zero) VW_TRY(s.in(approx, (size_t)B * N, &da));
-    VW_TRY(s.in<T>(nullptr, (size_t)B * N, &dy));
-    VW_TRY(inverse_impl<T>(c, dd, da, B, N, lo, hi, L, wid, boundary, J, detail_mask, approx_zero,
-                           flags & ~VW_FLAG_SYNC, dy, false, nullptr, 0));
-    VW_TRY(s.out(y, dy, (size_t)B * N));
-    VW_HIP(hipStreamSynchronize(c->stream));
+    VW_TRY(inverse_host<T>(c, details, B * N, approx, B, N, lo, hi, L, wid, boundary, J, detail_mask, approx_zero,
+                           flags, y));
     return ok();
   }
   VW_TRY(inverse_impl<T>(c, details, approx, B, N, lo, hi, L, wid, boundary, J, detail_mask, approx_zero, flags, y,
@@ -1433,6 +1495,90 @@ extern "C" vw_status vw_modwt_inverse_f32(vw_ctx* c, const float* details, const
                                           int J, unsigned detail_mask, int approx_zero, unsigned flags, float* y) {
   return modwt_inverse<float>(c, details, approx, B, N, lo, hi, L, wid, boundary, J, detail_mask, approx_zero, flags,
                               y);
+}
+
+// ------------------------------------------------------------------------------------------------
+// One batch over several contexts, one host thread per context ("each device has its
+// own context, stream, input generator and output buffers; one host thread per device").  The
+// reference parallelises one call in-process too (VectorWaveSwtAdapter.java:210-267 executor,
+// BatchMODWT.multiLevelAoS :90-111 over a batch); here the batch is split into contiguous row
+// blocks (vectorwave_amd/shard.py shard_rows: the first B % n blocks get one extra row) and block k
+// runs on ctxs[k] from its own std::thread -- no exchange between devices.  Host memory only (the
+// JNI / FFM caller's arrays): each thread stages its block through its context.
+static void shard_block(int64_t B, int n, int k, int64_t* start, int64_t* rows) {
+  const int64_t base = B / n, extra = B % n;
+  *start = k * base + std::min<int64_t>(k, extra);
+  *rows = base + (k < extra ? 1 : 0);
+}
+
+template <typename F>
+static vw_status run_sharded(vw_ctx* const* ctxs, int nctx, int64_t B, F&& fn) {
+  if (!ctxs) return fail(VW_ERR_NULL, "ctxs is null");
+  if (nctx < 1) return fail(VW_ERR_ARG, "need at least one context (got %d)", nctx);
+  for (int k = 0; k < nctx; ++k)
+    if (!ctxs[k]) return fail(VW_ERR_NULL, "ctxs[%d] is null", k);
+  if (B <= 0) return fail(VW_ERR_EMPTY, "batch must be non-empty (B=%lld)", (long long)B);
+  const int used = (int)std::min<int64_t>(nctx, B);
+  struct Res { vw_status st = VW_OK; std::string msg; int64_t idx = -1; };
+  std::vector<Res> res(used);
+  auto work = [&](int k) {
+    int64_t start, rows;
+    shard_block(B, used, k, &start, &rows);
+    const vw_status st = fn(ctxs[k], start, rows);
+    res[k].st = st;
+    if (st != VW_OK) { res[k].msg = t_err; res[k].idx = t_err_index; }
+  };
+  std::vector<std::thread> th;
+  th.reserve(used);
+  for (int k = 1; k < used; ++k) th.emplace_back(work, k);
+  work(0);
+  for (auto& t : th) t.join();
+  for (int k = 0; k < used; ++k)
+    if (res[k].st != VW_OK) {
+      t_err = "block " + std::to_string(k) + ": " + res[k].msg;
+      t_err_index = res[k].idx;
+      return res[k].st;
+    }
+  return ok();
+}
+
+extern "C" vw_status vw_modwt_forward_multi_f64(vw_ctx* const* ctxs, int nctx, const double* x, int64_t B, int64_t N,
+                                                int64_t ldx, const double* lo, const double* hi, int L, int wid,
+                                                int boundary, int J, unsigned flags, double* details,
+                                                double* approx) {
+  if (!(flags & VW_FLAG_HOST_MEMORY)) return fail(VW_ERR_ARG, "multi-context calls take host memory (VW_FLAG_HOST_MEMORY)");
+  if (!x || !details || !approx || !lo || !hi) return fail(VW_ERR_NULL, "null array argument");
+  if (ldx < N) return fail(VW_ERR_ARG, "ldx (%lld) < N (%lld)", (long long)ldx, (long long)N);
+  return run_sharded(ctxs, nctx, B, [&](vw_ctx* c, int64_t start, int64_t rows) -> vw_status {
+    (void)wid;
+    VW_TRY(check_common(c, x, details, lo, hi, rows, N, L, boundary));
+    VW_TRY(check_levels(N, L, J, flags));
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    hipSetDevice(c->device);
+    return forward_host<double>(c, x + start * ldx, rows, N, ldx, lo, hi, L, boundary, J, flags,
+                                details + start * N, B * N, approx + start * N);
+  });
+}
+
+extern "C" vw_status vw_modwt_inverse_multi_f64(vw_ctx* const* ctxs, int nctx, const double* details,
+                                                const double* approx, int64_t B, int64_t N, const double* lo,
+                                                const double* hi, int L, int wid, int boundary, int J,
+                                                unsigned detail_mask, int approx_zero, unsigned flags, double* y) {
+  if (!(flags & VW_FLAG_HOST_MEMORY)) return fail(VW_ERR_ARG, "multi-context calls take host memory (VW_FLAG_HOST_MEMORY)");
+  if (!y || !lo || !hi) return fail(VW_ERR_NULL, "null argument");
+  if (!details && detail_mask) return fail(VW_ERR_NULL, "details is null");
+  if (!approx && !approx_zero) return fail(VW_ERR_NULL, "approx is null");
+  if (J < 1 || J > kMaxLevels) return fail(VW_ERR_LEVEL, "levels must be in 1..%d", kMaxLevels);
+  if ((flags & VW_FLAG_CORE_LEVELS) && vw_upsampled_length(L, J) > N)
+    return fail(VW_ERR_TOO_LARGE, "Upsampled reconstruction filter length exceeds signal length");
+  return run_sharded(ctxs, nctx, B, [&](vw_ctx* c, int64_t start, int64_t rows) -> vw_status {
+    VW_TRY(check_common(c, y, y, lo, hi, rows, N, L, boundary));
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    hipSetDevice(c->device);
+    return inverse_host<double>(c, details ? details + start * N : nullptr, B * N,
+                                approx ? approx + start * N : nullptr, rows, N, lo, hi, L, wid, boundary, J,
+                                detail_mask, approx_zero, flags, y + start * N);
+  });
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -1,0 +1,114 @@
+"""One batch over several device contexts, one host thread per context.
+
+The reference parallelises a single batch call inside one JVM (BatchMODWT.multiLevelAoS over the
+batch, ext/extensions/modwt/BatchMODWT.java:90-111; the VectorWaveSwtAdapter executor,
+core/swt/VectorWaveSwtAdapter.java:210-267).  ``DeviceGroup`` is that call spread over GPUs: the batch
+is split into contiguous row blocks (``shard.shard_rows``), block k runs on context k from its own
+host thread, with no exchange between devices.
+
+* Host arrays (numpy, the JNI/FFM caller's ``double[][]``): one C call,
+  ``vw_modwt_forward_multi_f64`` / ``vw_modwt_inverse_multi_f64``, whose std::threads stage each
+  block through its own context.
+* Device tensors (one per context, already on that context's device): one Python thread per context
+  calling that context's engine.
+
+Contexts may share a device (several ``Engine`` instances on cuda:0 -- what the tests do on a one-GPU
+box) or sit on different devices.
+"""
+from __future__ import annotations
+
+import ctypes
+from concurrent.futures import ThreadPoolExecutor
+from ctypes import c_void_p
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as nat
+from .engine import Engine, _check
+from .errors import InvalidArgumentException
+from .shard import shard_rows
+from .wavelets import Wavelet
+
+
+class DeviceGroup:
+    """``DeviceGroup(devices=[0, 1, ...])``: one context per entry (repeat a device for several contexts
+    on it).  ``forward`` / ``inverse`` take a whole host batch and return whole host arrays."""
+
+    def __init__(self, devices: Sequence[int] = (0,), engines: Optional[List[Engine]] = None):
+        self.engines = list(engines) if engines else [Engine(d) for d in devices]
+        if not self.engines:
+            raise InvalidArgumentException("DeviceGroup needs at least one context")
+        self._own = engines is None
+        self._ctxs = (c_void_p * len(self.engines))(*[e.ctx.value for e in self.engines])
+
+    def __len__(self) -> int:
+        return len(self.engines)
+
+    def blocks(self, B: int):
+        """Row blocks [(start, rows)] in context order (min(len, B) of them)."""
+        n = min(len(self.engines), B)
+        return [shard_rows(B, n, k) for k in range(n)]
+
+    # -- host batch: one C call, one std::thread per context ------------------------------------
+    def forward(self, x, wavelet: Wavelet, levels: int, boundary: int = nat.PERIODIC, fma: bool = False,
+                core_levels: bool = False):
+        """x [B][N] host -> (details [J][B][N], approx [B][N]) host (BatchMODWT.multiLevelAoS semantics;
+        ``core_levels``: MultiLevelMODWTTransform's level cap)."""
+        a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+        if a.ndim != 2 or a.shape[0] == 0 or a.shape[1] == 0:
+            raise InvalidArgumentException("signals must be a non-empty [batch][length] array")
+        B, N = a.shape
+        det = np.empty((levels, B, N))
+        app = np.empty((B, N))
+        lo, hi = wavelet.lowPassDecomposition(), wavelet.highPassDecomposition()
+        flags = nat.FLAG_HOST_MEMORY | (nat.FLAG_FMA if fma else 0) | (nat.FLAG_CORE_LEVELS if core_levels else 0)
+        lib = nat.load()
+        _check(lib.vw_modwt_forward_multi_f64(self._ctxs, len(self.engines), a.ctypes.data_as(c_void_p), B, N, N,
+                                              nat.taps_array(lo), nat.taps_array(hi), len(lo), wavelet.wavelet_id,
+                                              boundary, levels, flags, det.ctypes.data_as(c_void_p),
+                                              app.ctypes.data_as(c_void_p)))
+        return det, app
+
+    def inverse(self, details, approx, wavelet: Wavelet, boundary: int = nat.PERIODIC, fma: bool = False):
+        """details [J][B][N], approx [B][N] host -> y [B][N] host (MultiLevelMODWTTransform.reconstruct)."""
+        d = np.ascontiguousarray(np.asarray(details, dtype=np.float64))
+        ap = np.ascontiguousarray(np.asarray(approx, dtype=np.float64))
+        if d.ndim != 3 or tuple(d.shape[1:]) != tuple(ap.shape):
+            raise InvalidArgumentException("details must be [levels][batch][length] matching approx")
+        J, B, N = d.shape
+        y = np.empty((B, N))
+        lo, hi = wavelet.lowPassReconstruction(), wavelet.highPassReconstruction()
+        flags = nat.FLAG_HOST_MEMORY | (nat.FLAG_FMA if fma else 0)
+        _check(nat.load().vw_modwt_inverse_multi_f64(self._ctxs, len(self.engines), d.ctypes.data_as(c_void_p),
+                                                     ap.ctypes.data_as(c_void_p), B, N, nat.taps_array(lo),
+                                                     nat.taps_array(hi), len(lo), wavelet.wavelet_id, boundary, J,
+                                                     0xFFFFFFFF, 0, flags, y.ctypes.data_as(c_void_p)))
+        return y
+
+    # -- device tensors: one Python thread per context ------------------------------------------
+    def forward_device(self, xs, wavelet: Wavelet, levels: int, boundary: int = nat.PERIODIC, fma: bool = False):
+        """xs: one [B_k][N] CUDA tensor per context (on that context's device) -> [(details, approx)]."""
+        if len(xs) != len(self.engines):
+            raise InvalidArgumentException("one tensor per context")
+        lo, hi = wavelet.lowPassDecomposition(), wavelet.highPassDecomposition()
+        fl = nat.FLAG_FMA if fma else 0
+
+        def one(k):
+            return self.engines[k].forward(xs[k], lo, hi, wavelet.wavelet_id, boundary, levels, fl)
+        with ThreadPoolExecutor(max_workers=len(self.engines)) as ex:
+            return list(ex.map(one, range(len(self.engines))))
+
+    def close(self) -> None:
+        if self._own:
+            for e in self.engines:
+                if e.ctx:
+                    _check(e.lib.vw_ctx_destroy(e.ctx))
+                    e.ctx = None
+        self.engines = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
