@@ -344,15 +344,15 @@ def test_forward_persistent_matches_per_signal_kernel(engine, case):
     x = torch.empty((B, n), dtype=dtype, device="cuda")
     engine.fill_uniform(x, 5)
     outs = []
-    for nv in (4, 8):
+    for nv in (4, 8, 2):
         for persist in (0, 1):
-            opts = dict(VW_FWD_PERSIST=persist, VW_NV=nv)
+            opts = dict(VW_FWD_PERSIST=persist, VW_NV=nv) if nv != 2 else dict(VW_FWD_PERSIST=persist, VW_FWD_NV=2)
             if buf:
                 opts["VW_FWD_BUF"] = int(buf)
             with engine.options(**opts):
                 outs.append(engine.forward(x, *lohi(w), w.wavelet_id, boundary, J, flags))
             torch.cuda.synchronize()
-    for d_, a_ in outs[2:]:  # the NV = 8 kernels (half the threads) compute the same bits
+    for d_, a_ in outs[2:]:  # the NV = 8 / NV = 2 kernels (half / twice the threads) compute the same bits
         assert torch.equal(d_, outs[0][0]) and torch.equal(a_, outs[0][1])
     outs = outs[:2]
     (d0, a0), (d1, a1) = outs
@@ -435,7 +435,8 @@ def test_multilevel_tiles_bit_exact(engine, tile):
 
 
 # ---- alternative fused inverse kernels (selected by policy or option) ------------------------------------
-@pytest.mark.parametrize("opts", [dict(VW_INV_BUF=1), dict(VW_INV_BUF=2), dict(VW_NV=8), dict(VW_INV_BUF=1, VW_NV=8)],
+@pytest.mark.parametrize("opts", [dict(VW_INV_BUF=1), dict(VW_INV_BUF=2), dict(VW_NV=8), dict(VW_INV_BUF=1, VW_NV=8),
+                                  dict(VW_INV_NV=2), dict(VW_INV_NV=2, VW_INV_BUF=1), dict(VW_INV_NV=2, VW_INV_BUF=2)],
                          ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
 @pytest.mark.parametrize("fma", [False, True], ids=["exact", "fma"])
 def test_inverse_kernel_variants_bit_exact(engine, opts, fma):

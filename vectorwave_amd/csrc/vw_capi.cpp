@@ -87,6 +87,8 @@ struct Tuning {
   int col_c = 0;               // VW_COL_C: residues per column block (0 = 64 bytes of samples)
   int col_tk = 0;              // VW_COL_TK: decimated positions per column tile (0 = the most that fit LDS)
   int col_threads = 1024;      // VW_COL_THREADS: workgroup size of the column-group forward
+  int fwd_nv = 0;              // VW_FWD_NV / VW_INV_NV = 2: 1024-thread fused kernels with 2 vectors per
+  int inv_nv = 0;              // thread (L <= 8, unrolled); 0 = policy
 };
 
 // One switch of the Tuning struct by its environment name; value < 0 = the default.  Returns false
@@ -117,6 +119,8 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_COL_C") t.col_c = v < 0 ? d.col_c : v;
   else if (k == "VW_COL_TK") t.col_tk = v < 0 ? d.col_tk : v;
   else if (k == "VW_COL_THREADS") t.col_threads = (v == 256 || v == 512 || v == 1024) ? v : d.col_threads;
+  else if (k == "VW_FWD_NV") t.fwd_nv = v < 0 ? d.fwd_nv : v;
+  else if (k == "VW_INV_NV") t.inv_nv = v < 0 ? d.inv_nv : v;
   else return false;
   return true;
 }
@@ -124,7 +128,8 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
 static const char* const kTuningKeys[] = {
     "VW_NV", "VW_FWD_PERSIST", "VW_FWD_BUF", "VW_FORCE_TILED", "VW_FWD_REV", "VW_INV_REV",
     "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_MULTI_PF", "VW_NO_SWEEP", "VW_SWEEP_QC",
-    "VW_UNROLL_MAX", "VW_BLK", "VW_COL", "VW_COL_MIN", "VW_COL_C", "VW_COL_TK", "VW_COL_THREADS"};
+    "VW_UNROLL_MAX", "VW_BLK", "VW_COL", "VW_COL_MIN", "VW_COL_C", "VW_COL_TK", "VW_COL_THREADS", "VW_FWD_NV",
+    "VW_INV_NV"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -706,10 +711,12 @@ static vw_status report_bad(unsigned long long bad, int64_t N) {
 // the unrolled kernels rely on slabs 0..NV-2 being full, `fit` = (NV-1)*threads <= nvec (else the
 // runtime-L kernel with a bounds check per vector runs).
 static bool fused_plan(const Tuning& tu, int64_t N, int V, int elem, int64_t lds_elems_extra, int* threads, int* nv,
-                       int* lds, bool* fit) {
+                       int* lds, bool* fit, int nv_req = 0) {
   const int64_t nvec = (N + V - 1) / V;
   int want = tu.nv;
   if ((nvec + want - 1) / want > 512) want = 8;  // NV = 4 kernels are bounded to 512 threads (VW_FUSED_BOUNDS)
+  // NV = 2: 1024 threads at most, every slab full (the unrolled kernels' contract)
+  if (nv_req == 2 && nvec % 2 == 0 && nvec / 2 <= kMaxThreads) want = 2;
   const int64_t th = (nvec + want - 1) / want;
   if (th > kMaxThreads) return false;
   const int64_t bytes = lds_elems_extra * elem;
@@ -885,11 +892,15 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
   const int64_t region = round_up(hlpad + nvec * V + V, V);
   bool dbl = tu.fwd_buf ? tu.fwd_buf == 2 : true;
   bool fused = false, fit = false;
+  // NV = 2 (1024-thread workgroups) only where the unrolled kernel will run (it has no runtime-L form)
+  const int fwd_nv2 = (tu.fwd_nv == 2 && io_aligned && L <= 8 && L <= tu.unroll_max && has_unrolled_taps(L) &&
+                       !(tu.blk > 0 && L >= tu.blk)) ? 2 : 0;
   if (J <= kMaxLevels && !tu.force_tiled) {
-    if (dbl) dbl = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
+    if (dbl) dbl = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit, fwd_nv2);
     if (dbl && !tu.fwd_buf && !fma && !persist_ok(threads, nv, fit)) dbl = false;  // EXACT without persistence
-    fused = dbl || fused_plan(tu, N, V, sizeof(T), region, &threads, &nv, &lds, &fit);
+    fused = dbl || fused_plan(tu, N, V, sizeof(T), region, &threads, &nv, &lds, &fit, fwd_nv2);
   }
+  if (fused && nv == 2 && !(fit && (int64_t)threads * 2 == nvec)) return fail(VW_ERR_STATE, "NV=2 plan without full slabs");
   if (fused) {
     for (int j = 0; j < J; ++j) set_halo_images(lv[j], N, npow2, V, threads, nv);
     FwdArgs<T> a;
@@ -912,7 +923,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     int blk_lds = 0;
     // (NV = 8: 1024-thread workgroups cap a lane at 128 VGPRs and the blocked forward spills there --
     // measured 2x slower at sym8 N = 16384; the one-vector-per-tap kernel runs instead)
-    if (tu.blk > 0 && L >= tu.blk && a.unrolled && !validate && !hist && (int64_t)threads * nv == nvec && nv <= 4) {
+    if (tu.blk > 0 && L >= tu.blk && a.unrolled && !validate && !hist && (int64_t)threads * nv == nvec && nv == 4) {
       bool okb = true;
       int hlv = 0;
       for (int j = 0; j < J; ++j) {
@@ -1143,11 +1154,13 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   const bool blk_pref = tu.blk > 0 && L >= tu.blk && boundary == VW_PERIODIC;
   bool db = !pair && (tu.inv_buf ? tu.inv_buf == 2 : (B <= 2LL * c->cus && !blk_pref));
   bool fused = false, fit = false;
+  const bool inv_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
+  const int inv_nv2 = (tu.inv_nv == 2 && inv_io && L <= 8 && L <= tu.unroll_max && has_unrolled_taps(L)) ? 2 : 0;
   if (!tu.force_tiled) {
-    if (pair || db) fused = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit);
+    if (pair || db) fused = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit, inv_nv2);
     if (!fused && !pair) {
       db = false;
-      fused = fused_plan(tu, N, V, sizeof(T), region, &threads, &nv, &lds, &fit);
+      fused = fused_plan(tu, N, V, sizeof(T), region, &threads, &nv, &lds, &fit, inv_nv2);
     }
   }
   if (fused) {
@@ -1162,7 +1175,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.thr_ld = thr_ld; a.soft = soft; a.taps = L;
     a.rev = tu.inv_rev;
     // register-blocked PERIODIC inverse for long filters (vw_device.h k_inverse_blk)
-    if (tu.blk > 0 && L >= tu.blk && !pair && !db && boundary == VW_PERIODIC && a.unrolled &&
+    if (tu.blk > 0 && L >= tu.blk && nv != 2 && !pair && !db && boundary == VW_PERIODIC && a.unrolled &&
         (int64_t)threads * nv == nvec) {
       bool okb = true;
       int64_t buf = 0;

@@ -668,9 +668,12 @@ __device__ __forceinline__ void zero_regs(T (&r)[NV][VT<T>::V]) {
 // signals): up to 1024 threads, 128 VGPRs.
 // Longer filters need wider register windows (the s = 1 window holds L + V - 1 values): L <= 8 gets
 // W waves, longer filters 4 (128 VGPRs; with 512-thread workgroups 5 waves would not add one).
+// NV = 2 (small batches: one 1024-thread workgroup per signal, two per CU = 8 waves per SIMD, 64 VGPRs):
+// twice the waves per signal where the batch leaves the CUs short of signals.
 #define VW_FUSED_W(L, W) ((L) <= 8 ? (W) : 4)
-#define VW_FUSED_BOUNDS(NV, W) \
-  __attribute__((amdgpu_flat_work_group_size(1, (NV) <= 4 ? 512 : 1024), amdgpu_waves_per_eu((NV) <= 4 ? (W) : 4)))
+#define VW_FUSED_BOUNDS(NV, W)                                                        \
+  __attribute__((amdgpu_flat_work_group_size(1, ((NV) <= 4 && (NV) != 2) ? 512 : 1024), \
+                 amdgpu_waves_per_eu((NV) == 2 ? 8 : (NV) <= 4 ? (W) : 4)))
 
 // ---------------------------------------------------------------------------------------------
 // Fused multi-level forward: MultiLevelMODWTTransform.decompose (:243-251) / BatchSIMDMODWT
@@ -944,8 +947,14 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_db(const InvArgs
 
 // Single-buffer sequential-sum form for signals too long for two LDS buffers: ONE region is
 // time-shared (a_j -> approx branch -> d_j -> detail branch -> a_{j-1}); four barriers per level.
+#ifndef VW_INV_LATE_PF
+#define VW_INV_LATE_PF 0
+#endif
+#ifndef VW_INV_W
+#define VW_INV_W 6  // waves per SIMD of k_inverse_seq (experiment builds: -DVW_INV_W=8 -> 64 VGPRs)
+#endif
 template <typename T, int L, bool FMA, int NV>
-__global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_seq(const InvArgs<T> p) {
+__global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, VW_INV_W)) k_inverse_seq(const InvArgs<T> p) {
   constexpr int V = VT<T>::V;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* R = reinterpret_cast<T*>(smem) + p.hlpad_a;
@@ -968,14 +977,22 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_seq(const InvArg
   for (int j = p.J; j >= 1; --j) {
     const LevelDesc lv = p.lv[j - 1];
     lds_barrier();  // R = a_j + halo
+#if VW_INV_LATE_PF
+    // (experiment) d_j issued at the start of level j, live only across the approximation branch
+    if (j < p.J)
+      load_row_regs<T, NV>(dreg, p.details + (size_t)(j - 1) * plane + b * (size_t)N, N, nvec, vec_ok,
+                           lv.use_d == 0);
+#endif
     zero_regs<T, NV>(acc);
     inv_row<T, L, FMA, NV>(R, nvec, lv.s, lv.dir_a, lv.off_a, p.lo, p.taps, acc);
     lds_barrier();  // every approximation-branch read done
     wait_vmem();    // the d_j prefetch
     regs_to_level<T, L, NV>(R, dreg, nvec, N, lv, 0, (const T*)nullptr, lv.use_d == 0, p.thr, thr_of(j), p.soft);
+#if !VW_INV_LATE_PF
     if (j > 1)
       load_row_regs<T, NV>(dreg, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, vec_ok,
                            p.lv[j - 2].use_d == 0);
+#endif
     lds_barrier();  // R = d_j + halo
     inv_row<T, L, FMA, NV>(R, nvec, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
     if (j > 1) {

@@ -17,6 +17,9 @@ static hipError_t run_forward_fused_nv(const FwdArgs<T>& a, int threads, int lds
 
 template <typename T, int L, bool FMA>
 static hipError_t run_forward_fused(const FwdArgs<T>& a, int threads, int lds, int nv, hipStream_t st) {
+  if constexpr (L > 0 && L <= 8) {  // NV = 2 (1024 threads): short filters at small batches (host policy)
+    if (nv == 2) return run_forward_fused_nv<T, L, FMA, 2>(a, threads, lds, st);
+  }
   return nv <= 4 ? run_forward_fused_nv<T, L, FMA, 4>(a, threads, lds, st) : run_forward_fused_nv<T, L, FMA, 8>(a, threads, lds, st);
 }
 

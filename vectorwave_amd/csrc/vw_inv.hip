@@ -9,9 +9,12 @@ static hipError_t run_inverse_fused_nv(const InvArgs<T>& a, int threads, int lds
   // pairwise sums: k_inverse_fused; sequential sums: two LDS buffers (k_inverse_db) or one (k_inverse_seq)
   static int configured_pair = 64 * 1024, configured_seq = 64 * 1024, configured_db = 64 * 1024,
              configured_blk = 64 * 1024;
-  const bool blk = L > 0 && a.blk && !a.pair && !a.db;  // register-blocked PERIODIC (host contract)
-  auto k = a.pair ? k_inverse_fused<T, L, FMA, NV> : a.db ? k_inverse_db<T, L, FMA, NV>
-         : blk    ? k_inverse_blk<T, (L > 0 ? L : 2), FMA, NV> : k_inverse_seq<T, L, FMA, NV>;
+  // register-blocked PERIODIC (host contract; never with NV = 2)
+  const bool blk = L > 0 && NV != 2 && a.blk && !a.pair && !a.db;
+  auto k = a.pair ? k_inverse_fused<T, L, FMA, NV> : a.db ? k_inverse_db<T, L, FMA, NV> : k_inverse_seq<T, L, FMA, NV>;
+  if constexpr (NV != 2) {
+    if (blk) k = k_inverse_blk<T, (L > 0 ? L : 2), FMA, NV>;
+  }
   hipError_t e = set_lds(k, lds, a.pair ? &configured_pair : a.db ? &configured_db
                                  : blk ? &configured_blk : &configured_seq);
   if (e != hipSuccess) return e;
@@ -21,6 +24,9 @@ static hipError_t run_inverse_fused_nv(const InvArgs<T>& a, int threads, int lds
 
 template <typename T, int L, bool FMA>
 static hipError_t run_inverse_fused(const InvArgs<T>& a, int threads, int lds, int nv, hipStream_t st) {
+  if constexpr (L > 0 && L <= 8) {  // NV = 2 (1024 threads): short filters at small batches (host policy)
+    if (nv == 2) return run_inverse_fused_nv<T, L, FMA, 2>(a, threads, lds, st);
+  }
   return nv <= 4 ? run_inverse_fused_nv<T, L, FMA, 4>(a, threads, lds, st) : run_inverse_fused_nv<T, L, FMA, 8>(a, threads, lds, st);
 }
 
