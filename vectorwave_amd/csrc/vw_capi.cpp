@@ -5,6 +5,7 @@
 // (vw_kernels.hip), or one tiled launch per level for signals longer than LDS holds.
 #include "../../include/vectorwave_amd.h"
 #include "vw_internal.h"
+#include "vw_deep.h"
 
 #include <algorithm>
 #include <cmath>
@@ -87,6 +88,13 @@ struct Tuning {
   int col_c = 0;               // VW_COL_C: residues per column block (0 = 64 bytes of samples)
   int col_tk = 0;              // VW_COL_TK: decimated positions per column tile (0 = the most that fit LDS)
   int col_threads = 1024;      // VW_COL_THREADS: workgroup size of the column-group forward
+  bool deep = true;             // VW_DEEP=0|1: streaming deep-level forward (vw_deep.hip) off / on
+  bool deep_inv = false;       // VW_DEEP_INV=1 (or VW_DEEP=1): the deep inverse too -- measured slower than
+                               // the column sweeps on db8-stream (profiles/r03/ab_deep_db8_stream.log)
+  int deep_lds = 80;           // VW_DEEP_LDS: LDS budget of one deep group, KiB (80 = two workgroups per CU)
+  int deep_waves = 4;          // VW_DEEP_WAVES: target deep workgroups per CU when choosing segments
+  int deep_pf_fwd = 1;         // VW_DEEP_PF_FWD / VW_DEEP_PF_INV: tiles of DMA-fed input in flight
+  int deep_pf_inv = 1;
   int fwd_nv = 0;              // VW_FWD_NV / VW_INV_NV = 2: 1024-thread fused kernels with 2 vectors per
   int inv_nv = 0;              // thread (L <= 8, unrolled); 0 = policy
 };
@@ -119,6 +127,12 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_COL_C") t.col_c = v < 0 ? d.col_c : v;
   else if (k == "VW_COL_TK") t.col_tk = v < 0 ? d.col_tk : v;
   else if (k == "VW_COL_THREADS") t.col_threads = (v == 256 || v == 512 || v == 1024) ? v : d.col_threads;
+  else if (k == "VW_DEEP") { t.deep = v < 0 ? d.deep : v != 0; t.deep_inv = v < 0 ? d.deep_inv : v != 0; }
+  else if (k == "VW_DEEP_INV") t.deep_inv = v < 0 ? d.deep_inv : v != 0;
+  else if (k == "VW_DEEP_LDS") t.deep_lds = v <= 0 ? d.deep_lds : v;
+  else if (k == "VW_DEEP_WAVES") t.deep_waves = v <= 0 ? d.deep_waves : v;
+  else if (k == "VW_DEEP_PF_FWD") t.deep_pf_fwd = v <= 0 ? d.deep_pf_fwd : std::min(v, 16);
+  else if (k == "VW_DEEP_PF_INV") t.deep_pf_inv = v <= 0 ? d.deep_pf_inv : std::min(v, 16);
   else if (k == "VW_FWD_NV") t.fwd_nv = v < 0 ? d.fwd_nv : v;
   else if (k == "VW_INV_NV") t.inv_nv = v < 0 ? d.inv_nv : v;
   else return false;
@@ -129,7 +143,7 @@ static const char* const kTuningKeys[] = {
     "VW_NV", "VW_FWD_PERSIST", "VW_FWD_BUF", "VW_FORCE_TILED", "VW_FWD_REV", "VW_INV_REV",
     "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_MULTI_PF", "VW_NO_SWEEP", "VW_SWEEP_QC",
     "VW_UNROLL_MAX", "VW_BLK", "VW_COL", "VW_COL_MIN", "VW_COL_C", "VW_COL_TK", "VW_COL_THREADS", "VW_FWD_NV",
-    "VW_INV_NV"};
+    "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -835,6 +849,62 @@ static bool col_plan(const Tuning& tu, const std::vector<LevelDesc>& lv, int j, 
   return true;
 }
 
+// Streaming deep group (vw_deep.hip): PERIODIC levels jlo..jhi of the per-level path in one launch.
+// Needs level jlo's spacing P to divide N and hold C = 64 bytes of residues; every ring of the group
+// within the LDS budget.  Ring capacities: DMA-fed rings hold their history + two tiles (the next
+// tile lands while the current one computes), multiples of 16 positions (one wave's DMA);
+// level-fed rings history + one tile.  Returns the LDS bytes, 0 if the group does not qualify.
+constexpr int kDeepTile = 128;  // vw_deep.hip kDeepT
+
+template <typename T>
+static int deep_plan(const Tuning& tu, const std::vector<LevelDesc>& lv, int jlo, int jhi, int L, int64_t N,
+                     bool inverse, DeepArgs<T>* a) {
+  constexpr int V = vec_width<T>();
+  const int C = 64 / (int)sizeof(T);
+  const int g = jhi - jlo + 1;
+  if (!(inverse ? tu.deep_inv : tu.deep) || g < 1 || g > kMaxGroup || !has_unrolled_taps(L)) return 0;
+  const int P = lv[jlo - 1].s;
+  if (P < C || P % C != 0 || N % P != 0 || N / P < 2 * kDeepTile) return 0;
+  for (int j = jlo; j <= jhi; ++j)
+    if (lv[j - 1].mode != kHaloPeriodic) return 0;
+  (void)V;
+  int caps[2 * kMaxGroup] = {}, nr = 0;
+  int64_t reach = 0;
+  const int D = inverse ? tu.deep_pf_inv : tu.deep_pf_fwd;
+  for (int k = 0; k < g; ++k) {
+    const int64_t H = (int64_t)(L - 1) << k;
+    reach += H;
+    const bool dma_fed = inverse ? (k == g - 1) : (k == 0);
+    caps[k] = dma_fed ? (int)round_up(H + (D + 1) * kDeepTile, 16) : (int)(H + kDeepTile);
+    if (inverse) caps[g + k] = (int)round_up(H + (D + 1) * kDeepTile, 16);
+  }
+  nr = inverse ? 2 * g : g;
+  int64_t pos = 0;
+  for (int r = 0; r < nr; ++r) pos += caps[r];
+  const int64_t bytes = pos * 64;
+  if (bytes > (int64_t)tu.deep_lds * 1024 || bytes > kLdsBytes) return 0;
+  if (a) {
+    a->P = P; a->C = C; a->nq = (int)(N / P); a->nb = P / C; a->g = g; a->N = (int)N;
+    a->warm = (int)round_up(reach, kDeepTile);
+    a->depth = D;
+    int64_t o = 0;
+    for (int r = 0; r < nr; ++r) { a->cap[r] = caps[r]; a->off[r] = (int)(o * C); o += caps[r]; }
+  }
+  return (int)bytes;
+}
+
+// Segments per residue block: enough workgroups for `deep_waves` per CU, each segment at least four
+// warm-ups long (the warm-up is recomputed per segment).
+template <typename T>
+static void deep_segments(const Tuning& tu, int cus, int64_t B, DeepArgs<T>* a) {
+  const int64_t wg0 = B * a->nb;
+  int64_t seg = std::max<int64_t>(1, ((int64_t)tu.deep_waves * cus + wg0 - 1) / wg0);
+  seg = std::min<int64_t>(seg, std::max<int64_t>(1, a->nq / (4 * (int64_t)a->warm)));
+  a->seg = (int)seg;
+  a->seglen = (int)round_up((a->nq + seg - 1) / seg, kDeepTile);
+  a->seg = (int)((a->nq + a->seglen - 1) / a->seglen);
+}
+
 // ------------------------------------------------------------------------------------------------
 // Forward (multi-level and single-level share this path).
 template <typename T>
@@ -980,6 +1050,30 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     const std::vector<int> groups = level_groups(tu, lv, J, L, V, mtile, !validate && !hist);
     for (int j = 1; j <= J; ++j) {
       T* const nxt = (src == tmp[0]) ? tmp[1] : tmp[0];  // never the level's own input
+      // streaming deep group from level j: the longest run j..je within the LDS budget
+      if (groups[j - 1] == 1 && !validate && !hist && (lda % V) == 0 && aligned16(src) && aligned16(details) &&
+          aligned16(approx) && deep_plan<T>(tu, lv, j, j, L, N, false, nullptr)) {
+        int je = j;
+        while (je < J && groups[je] == 1 && deep_plan<T>(tu, lv, j, je + 1, L, N, false, nullptr)) ++je;
+        DeepArgs<T> d;
+        memset(&d, 0, sizeof(d));
+        const int lds = deep_plan<T>(tu, lv, j, je, L, N, false, &d);
+        deep_segments<T>(tu, c->cus, B, &d);
+        d.src = src; d.lda = lda; d.B = B; d.taps = L;
+        d.out = (je == J) ? approx : nxt;
+        for (int k = 0; k < d.g; ++k) d.out_d[k] = details + (size_t)(j - 1 + k) * plane;
+        copy_taps(d.lo, lo, L);
+        copy_taps(d.hi, hi, L);
+        {
+          LaunchTimer lt(c, "forward_level");
+          hipError_t e = launch_deep<T>(d, lds, fma, false, c->stream);
+          if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward deep launch failed: %s", hipGetErrorString(e));
+        }
+        src = d.out;
+        lda = N;
+        j = je;
+        continue;
+      }
       ColPlan cp;
       if (groups[j - 1] == 1 && (lda % V) == 0 &&
           col_plan(tu, lv, j, J, L, V, N, (int)sizeof(T), !validate && !hist, &cp)) {
@@ -1247,8 +1341,38 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
           jc = j;
       }
     }
+    std::vector<char> in_group(J + 1, 0);  // levels inside a multi-level tile group
+    for (int e = 1; e <= J; ++e)
+      for (int k = start_of[e]; start_of[e] > 0 && k <= e; ++k) in_group[k] = 1;
     for (int j = J; j >= 1; --j) {
       T* const nxt = (cur == tmp[0]) ? tmp[1] : tmp[0];  // never the level's own input
+      // streaming deep group with top level j: the lowest jl whose group jl..j fits the LDS budget
+      if (!pair && boundary == VW_PERIODIC && !in_group[j] && aligned16(cur) && aligned16(details) &&
+          aligned16(y) && deep_plan<T>(tu, lv, j, j, L, N, true, nullptr)) {
+        int jl = j;
+        while (jl > 1 && !in_group[jl - 1] && deep_plan<T>(tu, lv, jl - 1, j, L, N, true, nullptr)) --jl;
+        DeepArgs<T> d;
+        memset(&d, 0, sizeof(d));
+        const int lds = deep_plan<T>(tu, lv, jl, j, L, N, true, &d);
+        deep_segments<T>(tu, c->cus, B, &d);
+        d.src = cur; d.lda = N; d.B = B; d.taps = L; d.soft = soft;
+        d.out = (jl == 1) ? y : nxt;
+        for (int k = 0; k < d.g; ++k) {
+          const LevelDesc& ld = lv[jl - 1 + k];
+          d.src_d[k] = ld.use_d ? details + (size_t)(jl - 1 + k) * plane : nullptr;
+          d.thr[k] = thr ? thr + (size_t)(jl - 1 + k) * (size_t)thr_ld : nullptr;
+        }
+        copy_taps(d.lo, lo, L);
+        copy_taps(d.hi, hi, L);
+        {
+          LaunchTimer lt(c, "inverse_level");
+          hipError_t e = launch_deep<T>(d, lds, fma, true, c->stream);
+          if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse deep launch failed: %s", hipGetErrorString(e));
+        }
+        cur = d.out;
+        j = jl;
+        continue;
+      }
       if (jc && j == J) {
         MultiArgs<T> m;
         memset(&m, 0, sizeof(m));

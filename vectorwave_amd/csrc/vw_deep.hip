@@ -1,0 +1,441 @@
+// vw_deep.hip -- streaming deep-level kernels (instantiation unit, once per element type).
+//
+// The deep PERIODIC levels j0..J of a long signal (BatchStreamingMODWT's 2^20-sample blocks at db8
+// J = 10: levels 6..10) in ONE launch each way, each input read from HBM once and each output written
+// once.  Level j0's spacing P = 2^(j0-1) divides N, so from level j0 on the cascade never mixes the
+// residue classes mod P: in the decimated coordinate q (sample t = q*P + r) level j0+k is a dense
+// L-tap filter with spacing 2^k (MultiLevelMODWTTransform.java:243-251 forward, :339-349 / :576-589
+// inverse; ScalarOps.java:700-723 circular convolution).
+//
+// A workgroup owns C consecutive residues (64 contiguous bytes per decimated position) of one signal
+// and STREAMS along q in tiles of kDeepT positions.  Every level keeps, in an LDS ring, the part of its
+// input that the coming tiles still read (its history of (L-1)*2^k positions) plus the current tile,
+// so nothing is re-read or recomputed between tiles -- the column sweeps read and write three rows per
+// level (2.1x the group's algorithmic bytes at db8 levels 6..10), the earlier column-group tiles
+// re-read their whole reach per tile.  The next tile's input arrives by LDS-DMA
+// (global_load_lds_dwordx4) `depth` tiles ahead of the computing one: one tile of 4 KiB in flight per
+// workgroup left every tile waiting for its load (measured: slower than the sweeps).
+//
+// Periodic boundary: the stream starts `warm` positions before the segment (wrapping mod N/P) and
+// stores nothing there; after that warm-up every ring holds exactly the values the reference's
+// modulo index would read (the group's reach is sum_k (L-1)*2^k positions).  Outputs computed from
+// the not-yet-valid start of a ring are never stored (the reach argument), so uninitialised LDS is
+// harmless.  Per output the taps run in the reference's order (forward: i ascending, both filters
+// from one read; inverse: approximation branch then detail branch) -> bit-exact in EXACT mode.
+#include "vw_launch.h"
+#include "vw_deep.h"
+#include <algorithm>
+
+namespace vw {
+
+constexpr int kDeepNP = 2;                // positions per thread
+constexpr int kDeepT = 64 * kDeepNP;      // decimated positions per tile (256 threads = 64 x 4 chunks)
+
+// Global stores of the deep kernels (experiment builds: -DVW_DEEP_STORE=0 none, 2 plain; default 1
+// non-temporal)
+#ifndef VW_DEEP_STORE
+#define VW_DEEP_STORE 1
+#endif
+template <typename vec, typename T>
+__device__ __forceinline__ void deep_store(T* dst, const vec& v) {
+  if constexpr (VW_DEEP_STORE == 1) __builtin_nontemporal_store(v, reinterpret_cast<vec*>(dst));
+  else if constexpr (VW_DEEP_STORE == 2) *reinterpret_cast<vec*>(dst) = v;
+}
+constexpr int kDeepThreads = 256;
+
+// One wave's LDS-DMA of 16 positions x 64 bytes (1 KiB): lane -> position lane / 4, 16-byte chunk lane % 4.
+template <typename T>
+__device__ __forceinline__ void deep_dma(T* lds_dst, const T* __restrict__ gsrc) {
+  const unsigned lds = (unsigned)(uintptr_t)lds_dst;
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(lds))
+      : "memory");
+}
+
+// vmcnt(n) for a wave-uniform runtime n (0..63; larger waits for 63, i.e. for more)
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+  switch (n) {
+    case 0: wait_vmcnt<0>(); break;
+    case 1: wait_vmcnt<1>(); break;
+    case 2: wait_vmcnt<2>(); break;
+    case 3: wait_vmcnt<3>(); break;
+    case 4: wait_vmcnt<4>(); break;
+    case 5: wait_vmcnt<5>(); break;
+    case 6: wait_vmcnt<6>(); break;
+    case 7: wait_vmcnt<7>(); break;
+    case 8: wait_vmcnt<8>(); break;
+    case 9: wait_vmcnt<9>(); break;
+    case 10: wait_vmcnt<10>(); break;
+    case 11: wait_vmcnt<11>(); break;
+    case 12: wait_vmcnt<12>(); break;
+    case 13: wait_vmcnt<13>(); break;
+    case 14: wait_vmcnt<14>(); break;
+    case 15: wait_vmcnt<15>(); break;
+    case 16: wait_vmcnt<16>(); break;
+    case 17: wait_vmcnt<17>(); break;
+    case 18: wait_vmcnt<18>(); break;
+    case 19: wait_vmcnt<19>(); break;
+    case 20: wait_vmcnt<20>(); break;
+    case 21: wait_vmcnt<21>(); break;
+    case 22: wait_vmcnt<22>(); break;
+    case 23: wait_vmcnt<23>(); break;
+    case 24: wait_vmcnt<24>(); break;
+    case 25: wait_vmcnt<25>(); break;
+    case 26: wait_vmcnt<26>(); break;
+    case 27: wait_vmcnt<27>(); break;
+    case 28: wait_vmcnt<28>(); break;
+    case 29: wait_vmcnt<29>(); break;
+    case 30: wait_vmcnt<30>(); break;
+    case 31: wait_vmcnt<31>(); break;
+    case 32: wait_vmcnt<32>(); break;
+    case 33: wait_vmcnt<33>(); break;
+    case 34: wait_vmcnt<34>(); break;
+    case 35: wait_vmcnt<35>(); break;
+    case 36: wait_vmcnt<36>(); break;
+    case 37: wait_vmcnt<37>(); break;
+    case 38: wait_vmcnt<38>(); break;
+    case 39: wait_vmcnt<39>(); break;
+    case 40: wait_vmcnt<40>(); break;
+    case 41: wait_vmcnt<41>(); break;
+    case 42: wait_vmcnt<42>(); break;
+    case 43: wait_vmcnt<43>(); break;
+    case 44: wait_vmcnt<44>(); break;
+    case 45: wait_vmcnt<45>(); break;
+    case 46: wait_vmcnt<46>(); break;
+    case 47: wait_vmcnt<47>(); break;
+    case 48: wait_vmcnt<48>(); break;
+    case 49: wait_vmcnt<49>(); break;
+    case 50: wait_vmcnt<50>(); break;
+    case 51: wait_vmcnt<51>(); break;
+    case 52: wait_vmcnt<52>(); break;
+    case 53: wait_vmcnt<53>(); break;
+    case 54: wait_vmcnt<54>(); break;
+    case 55: wait_vmcnt<55>(); break;
+    case 56: wait_vmcnt<56>(); break;
+    case 57: wait_vmcnt<57>(); break;
+    case 58: wait_vmcnt<58>(); break;
+    case 59: wait_vmcnt<59>(); break;
+    case 60: wait_vmcnt<60>(); break;
+    case 61: wait_vmcnt<61>(); break;
+    case 62: wait_vmcnt<62>(); break;
+    case 63: wait_vmcnt<63>(); break;
+    default: wait_vmcnt<63>(); break;
+  }
+}
+
+// Prefetch bookkeeping (per wave; every quantity is wave-uniform).  Event order: the prologue issues the
+// DMA batches of tiles 0..D-1; tile tau issues the batch of tile tau + D (if it exists), then st(tau)
+// stores.  Before tile tn computes, its batch must have landed: the wave waits until at most the
+// vector-memory operations issued AFTER that batch are outstanding (vmcnt retires in issue order).
+struct DeepPf {
+  int D, nt, ndma, nst, warm_tiles;
+  __device__ __forceinline__ int st(int tau) const { return tau >= warm_tiles ? nst : 0; }
+  __device__ __forceinline__ int after(int tn, int t) const {  // ops issued after tile tn's batch, by the end of tile t
+    int n = 0, tau0;
+    if (tn < D) {
+      n += (min(D, nt) - 1 - tn) * ndma;  // later prologue batches
+      tau0 = 0;
+    } else {
+      n += st(tn - D);                    // the stores of the tile that issued it
+      tau0 = tn - D + 1;
+    }
+    for (int tau = tau0; tau <= t; ++tau) n += (tau + D < nt ? ndma : 0) + st(tau);
+    return n;
+  }
+};
+
+// Workgroup -> (signal b, residue block rb, segment sg).  The nb residue blocks of one (b, sg) read and
+// write interleaved 64-byte pieces of the same 128-byte lines: they go to the same XCD (blockIdx % 8)
+// so those lines meet in one L2.  Returns false for the padding workgroups of the rounded grid.
+struct DeepWork {
+  long long b;
+  int rb, sg;
+};
+
+__device__ __forceinline__ bool deep_work(long long B, int nb, int seg, DeepWork* w) {
+  const long long id = blockIdx.x;
+  const long long xcd = id & 7, slot = id >> 3;
+  const long long gi = (slot / nb) * 8 + xcd;  // (b, sg) group
+  if (gi >= B * seg) return false;
+  w->rb = (int)(slot % nb);
+  w->b = gi / seg;
+  w->sg = (int)(gi % seg);
+  return true;
+}
+
+__device__ __forceinline__ int ring_wrap(int s, int cap) { return s < 0 ? s + cap : (s >= cap ? s - cap : s); }
+
+// ---------------------------------------------------------------------------------------------------
+// Thread mapping: thread tid owns the 16-byte chunk (tid & 3) of the C residues at the kDeepNP
+// positions pi + 64 r (pi = tid >> 2) of a tile: kDeepNP independent accumulators per branch and
+// element keep the dependent FMA chains of the few resident waves overlapped.  Ring slots are derived
+// from a workgroup-uniform base per tile and level (one compare per tap, no integer division).
+
+// Forward: level j0+k reads its input at q - i*2^k (left reach), so the stream runs q ascending.
+// Ring k holds level j0+k's input; ring 0 is fed by LDS-DMA, `depth` tiles ahead (capacity >= history +
+// (depth + 1) tiles, a multiple of 16), ring k+1 by level k's approximation.
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(kDeepThreads) k_forward_deep(const DeepArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  constexpr int C = 64 / (int)sizeof(T);
+  constexpr int NP = kDeepNP;
+  using vec = typename VT<T>::v;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* const lds = reinterpret_cast<T*>(smem);
+  DeepWork wk;
+  if (!deep_work(p.B, p.nb, p.seg, &wk)) return;
+  const int P = p.P, nq = p.nq, g = p.g;
+  const int tid = threadIdx.x;
+  const int pi = tid >> 2;                  // first position within the tile
+  const int ce = (tid & 3) * V;             // element offset within the C residues
+  const int wave = tid >> 6, lane = tid & 63;
+  const long long rowoff = wk.b * (long long)p.N + (long long)wk.rb * C;
+  const T* __restrict__ src = p.src + wk.b * p.lda + (long long)wk.rb * C;
+  const int qs = wk.sg * p.seglen;
+  const int qe = min(qs + p.seglen, nq);
+  const int total = p.warm + (qe - qs);     // positions streamed
+  const int nt = (total + kDeepT - 1) / kDeepT;
+  int qst = (qs - p.warm) % nq;             // q of stream position 0
+  if (qst < 0) qst += nq;
+  auto qwrap = [&](int q) { return q >= nq ? q - nq : q; };
+  auto q_tile = [&](int u0) { return (int)(((long long)qst + u0) % nq); };  // uniform
+  // this wave's share of a tile's DMA: 16-position chunks wave + 4m, lane -> position lane / 4
+  auto dma_tile = [&](int u0) {
+    const int s0 = u0 % p.cap[0], q0 = q_tile(u0);
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      const int c16 = 16 * (wave + 4 * m);
+      const int q = qwrap(q0 + c16 + (lane >> 2));
+      const int sl = s0 + c16 >= p.cap[0] ? s0 + c16 - p.cap[0] : s0 + c16;  // caps are multiples of 16
+      deep_dma<T>(lds + p.off[0] + sl * C, src + (long long)q * P + (lane & 3) * V);
+    }
+  };
+  DeepPf pf{p.depth, nt, NP, NP * (g + 1), p.warm / kDeepT};
+  for (int i = 0; i < min(pf.D, nt); ++i) dma_tile(i * kDeepT);  // prologue: D tiles in flight
+  wait_vmcnt_rt(pf.after(0, -1));
+  lds_barrier();
+  for (int t = 0; t < nt; ++t) {
+    const int u0 = t * kDeepT;
+    if (t + pf.D < nt) dma_tile(u0 + pf.D * kDeepT);  // ring 0: tile t + D, in flight across D tiles
+    const bool store = u0 >= p.warm;                   // tile-uniform; the last tile's tail is masked
+    const int q0 = q_tile(u0);
+    long long gofs[NP];
+    bool live[NP];
+#pragma unroll
+    for (int r = 0; r < NP; ++r) {
+      gofs[r] = rowoff + (long long)qwrap(q0 + pi + 64 * r) * P + ce;
+      live[r] = store && u0 + pi + 64 * r < total;
+    }
+    for (int k = 0; k < g; ++k) {
+      if (k > 0) lds_barrier();  // ring k holds level k-1's approximation of this tile
+      const int cap = p.cap[k], sk = 1 << k;
+      const T* ring = lds + p.off[k] + ce;
+      const int s0 = u0 % cap;
+      int br[NP];
+#pragma unroll
+      for (int r = 0; r < NP; ++r) {
+        const int v = s0 + pi + 64 * r;
+        br[r] = v >= cap ? v - cap : v;
+      }
+      T al[NP][V], ah[NP][V];
+#pragma unroll
+      for (int r = 0; r < NP; ++r)
+#pragma unroll
+        for (int e = 0; e < V; ++e) { al[r][e] = T(0); ah[r][e] = T(0); }
+#pragma unroll
+      for (int i = 0; i < L; ++i) {
+#pragma unroll
+        for (int r = 0; r < NP; ++r) {
+          int sl = br[r] - i * sk;
+          sl = sl < 0 ? sl + cap : sl;
+          const vec x = *reinterpret_cast<const vec*>(ring + sl * C);
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            al[r][e] = madd<FMA>(al[r][e], x[e], p.lo[i]);
+            ah[r][e] = madd<FMA>(ah[r][e], x[e], p.hi[i]);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < NP; ++r)
+#pragma unroll
+        for (int e = 0; e < V; ++e) {  // both chains computed here, not sunk into the store branch
+          asm volatile("" : "+v"(al[r][e]));
+          asm volatile("" : "+v"(ah[r][e]));
+        }
+      const int cap1 = k + 1 < g ? p.cap[k + 1] : 1;
+      const int s1 = u0 % cap1;
+#pragma unroll
+      for (int r = 0; r < NP; ++r) {
+        vec od, oa;
+#pragma unroll
+        for (int e = 0; e < V; ++e) { od[e] = ah[r][e]; oa[e] = al[r][e]; }
+        if (live[r]) deep_store<vec>(p.out_d[k] + gofs[r], od);
+        if (k + 1 < g) {
+          const int v = s1 + pi + 64 * r;
+          *reinterpret_cast<vec*>(lds + p.off[k + 1] + (v >= cap1 ? v - cap1 : v) * C + ce) = oa;
+        } else if (live[r]) {
+          deep_store<vec>(p.out + gofs[r], oa);
+        }
+      }
+    }
+    // tile t+1's batch has landed once at most the operations issued after it are outstanding
+    if (t + 1 < nt) wait_vmcnt_rt(pf.after(t + 1, t));
+    lds_barrier();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------------
+// Inverse: level j0+k reads a and d at q + i*2^k (right reach), so the stream runs q DESCENDING:
+// stream position u = 0, 1, ... is q = qe - 1 + warm - u, and "history" is the larger q.  Rings:
+// A_k (approximation input of level j0+k; A_{g-1} = a_J fed by DMA, A_k for k < g-1 by level k+1's
+// output) and D_k (d of level j0+k, fed by DMA `depth` tiles ahead).  DMA-fed rings have capacity >=
+// history + (depth + 1) tiles.  A descending chunk of 16 positions is still written to 16 ascending
+// slots by the DMA, so positions map to slots through u (not q).
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(kDeepThreads) k_inverse_deep(const DeepArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  constexpr int C = 64 / (int)sizeof(T);
+  constexpr int NP = kDeepNP;
+  using vec = typename VT<T>::v;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* const lds = reinterpret_cast<T*>(smem);
+  DeepWork wk;
+  if (!deep_work(p.B, p.nb, p.seg, &wk)) return;
+  const int P = p.P, nq = p.nq, g = p.g;
+  const int tid = threadIdx.x;
+  const int pi = tid >> 2;
+  const int ce = (tid & 3) * V;
+  const int wave = tid >> 6, lane = tid & 63;
+  const long long cofs = wk.b * (long long)p.N + (long long)wk.rb * C;
+  const int qs = wk.sg * p.seglen;
+  const int qe = min(qs + p.seglen, nq);
+  const int total = p.warm + (qe - qs);
+  const int nt = (total + kDeepT - 1) / kDeepT;
+  const int qst = (int)(((long long)qe - 1 + p.warm) % nq);   // q of stream position 0
+  auto qdown = [&](int q) { return q < 0 ? q + nq : q; };
+  auto q_tile = [&](int u0) { return (int)((((long long)qst - u0) % nq + nq) % nq); };
+  auto dma_ring = [&](int rg, const T* row, int u0, int s0, int q0) {
+#pragma unroll
+    for (int m = 0; m < NP; ++m) {
+      const int c16 = 16 * (wave + 4 * m);
+      const int q = qdown(q0 - c16 - (lane >> 2));
+      const int sl = s0 + c16 >= p.cap[rg] ? s0 + c16 - p.cap[rg] : s0 + c16;  // caps are multiples of 16
+      deep_dma<T>(lds + p.off[rg] + sl * C, row + cofs + (long long)q * P + (lane & 3) * V);
+    }
+  };
+  // ring indices: A_k = k, D_k = g + k
+  auto dma_tile = [&](int u0) {
+    const int q0 = q_tile(u0);
+    if (p.src) dma_ring(g - 1, p.src, u0, u0 % p.cap[g - 1], q0);
+    for (int k = 0; k < g; ++k)
+      if (p.src_d[k]) dma_ring(g + k, p.src_d[k], u0, u0 % p.cap[g + k], q0);
+  };
+  int nring = p.src ? 1 : 0;
+  for (int k = 0; k < g; ++k) nring += p.src_d[k] ? 1 : 0;
+  DeepPf pf{p.depth, nt, NP * nring, NP, p.warm / kDeepT};
+  for (int i = 0; i < min(pf.D, nt); ++i) dma_tile(i * kDeepT);
+  wait_vmcnt_rt(pf.after(0, -1));
+  lds_barrier();
+  for (int t = 0; t < nt; ++t) {
+    const int u0 = t * kDeepT;
+    if (t + pf.D < nt) dma_tile(u0 + pf.D * kDeepT);
+    const bool store = u0 >= p.warm;
+    const int q0 = q_tile(u0);
+    for (int k = g - 1; k >= 0; --k) {
+      if (k < g - 1) lds_barrier();  // A_k holds level k+1's output of this tile
+      const int sk = 1 << k;
+      T acc[NP][V];
+#pragma unroll
+      for (int r = 0; r < NP; ++r)
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc[r][e] = T(0);
+      // approximation branch (all taps), then detail branch: MultiLevelMODWTTransform.java:576-589
+      auto branch = [&](int rg, const T* f, bool thr_on, T thr_b) {
+        const int cap = p.cap[rg];
+        const T* ring = lds + p.off[rg] + ce;
+        const int s0 = u0 % cap;
+        int br[NP];
+#pragma unroll
+        for (int r = 0; r < NP; ++r) {
+          const int v = s0 + pi + 64 * r;
+          br[r] = v >= cap ? v - cap : v;
+        }
+#pragma unroll
+        for (int i = 0; i < L; ++i) {
+#pragma unroll
+          for (int r = 0; r < NP; ++r) {
+            int sl = br[r] - i * sk;
+            sl = sl < 0 ? sl + cap : sl;
+            const vec x = *reinterpret_cast<const vec*>(ring + sl * C);
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+              acc[r][e] = madd<FMA>(acc[r][e], thr_on ? threshold_t(x[e], thr_b, p.soft) : x[e], f[i]);
+          }
+        }
+      };
+      if (k < g - 1 || p.src) branch(k, p.lo, false, T(0));
+      if (p.src_d[k]) {
+        if (p.thr[k]) branch(g + k, p.hi, true, load_uniform(p.thr[k] + wk.b));
+        else branch(g + k, p.hi, false, T(0));
+      }
+      if (k > 0) {
+        const int cap1 = p.cap[k - 1];
+        const int s1 = u0 % cap1;
+#pragma unroll
+        for (int r = 0; r < NP; ++r) {
+          vec o;
+#pragma unroll
+          for (int e = 0; e < V; ++e) o[e] = acc[r][e];
+          const int v = s1 + pi + 64 * r;
+          *reinterpret_cast<vec*>(lds + p.off[k - 1] + (v >= cap1 ? v - cap1 : v) * C + ce) = o;
+        }
+      } else if (store) {
+#pragma unroll
+        for (int r = 0; r < NP; ++r) {
+          vec o;
+#pragma unroll
+          for (int e = 0; e < V; ++e) o[e] = acc[r][e];
+          if (u0 + pi + 64 * r < total) deep_store<vec>(p.out + cofs + (long long)qdown(q0 - pi - 64 * r) * P + ce, o);
+        }
+      }
+    }
+    if (t + 1 < nt) wait_vmcnt_rt(pf.after(t + 1, t));
+    lds_barrier();
+  }
+}
+
+template <typename T, int L, bool FMA, bool INV>
+static hipError_t run_deep(const DeepArgs<T>& a, int lds, hipStream_t st) {
+  auto k = INV ? k_inverse_deep<T, L, FMA> : k_forward_deep<T, L, FMA>;
+  static int configured = 64 * 1024;
+  hipError_t e = set_lds(k, lds, &configured);
+  if (e != hipSuccess) return e;
+  const long long groups = (a.B * a.seg + 7) / 8 * 8;
+  hipLaunchKernelGGL(k, dim3((unsigned)(groups * a.nb)), dim3(kDeepThreads), lds, st, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_deep(const DeepArgs<T>& a, int lds_bytes, bool fma, bool inverse, hipStream_t st) {
+  switch (a.taps) {
+#define VW_CASE(n)                                                                                    \
+    case n:                                                                                           \
+      if (inverse) return fma ? run_deep<T, n, true, true>(a, lds_bytes, st) : run_deep<T, n, false, true>(a, lds_bytes, st); \
+      return fma ? run_deep<T, n, true, false>(a, lds_bytes, st) : run_deep<T, n, false, false>(a, lds_bytes, st);
+    VW_TAP_LIST(VW_CASE)
+#undef VW_CASE
+    default:
+      return hipErrorNotSupported;
+  }
+}
+template hipError_t launch_deep<VW_T>(const DeepArgs<VW_T>&, int, bool, bool, hipStream_t);
+
+}  // namespace vw
