@@ -2,8 +2,9 @@
 
 MODWT/SWT signals are independent, so a batch splits into contiguous row blocks with
 no exchange on the data path: rank r of `world` transforms rows [start, start + count) of the global
-batch on its own device.  Used by bench.py (weak scaling: each rank owns B rows of a world*B batch)
-and by callers that split one large batch (strong scaling).
+batch on its own device.  Used by bench.py (strong scaling, the headline: the GLOBAL batch split into
+contiguous blocks; its weak-scaling line gives every rank a full batch) and by DeviceGroup, whose C
+entry points (vw_modwt_forward_multi_f64) split the same way in one process.
 """
 
 
