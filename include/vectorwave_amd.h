@@ -304,6 +304,11 @@ VW_API vw_status vw_memcpy(vw_ctx *ctx, void *dst, const void *src, int64_t byte
 VW_API vw_status vw_ctx_enable_timing(vw_ctx *ctx, int enable);
 VW_API vw_status vw_ctx_kernel_time(vw_ctx *ctx, const char *family, double *total_ms, int64_t *launches);
 VW_API vw_status vw_ctx_reset_timing(vw_ctx *ctx);
+/* Start / end (ms after ref_event, a hipEvent_t recorded earlier on any stream of the device) of the
+ * timed launches of `family` not yet collected by vw_ctx_kernel_time: the wall window of a kernel
+ * family when several contexts run concurrently.  *count = launches found (at most max written). */
+VW_API vw_status vw_ctx_kernel_spans(vw_ctx *ctx, const char *family, void *ref_event, int64_t max,
+                                     double *start_ms, double *end_ms, int64_t *count);
 
 #ifdef __cplusplus
 }

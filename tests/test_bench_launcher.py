@@ -43,8 +43,10 @@ def test_launcher_uneven_batch():
 
 def test_no_collective_inside_timed_interval():
     """bench.measure() on fakes that log every call: between the start of the clock (perf_counter + the
-    opening HIP event) and its end (closing event + synchronize + perf_counter) only the replay of the
-    K recorded steps runs -- the barriers of the contract lie outside."""
+    opening HIP event on the main stream) and its end (closing event + synchronize + perf_counter) only
+    the fork to the contexts' streams, their graph replays and the join run -- the barriers of the
+    contract lie outside."""
+    import contextlib
     sys.path.insert(0, ROOT)
     import bench
 
@@ -52,13 +54,17 @@ def test_no_collective_inside_timed_interval():
 
     class Ev:
         def __init__(self, **kw):
-            self.name = None
+            pass
 
-        def record(self):
+        def record(self, stream=None):
             log.append("event")
 
         def elapsed_time(self, other):
             return 1.0
+
+    class Stream:
+        def wait_event(self, e):
+            log.append("wait")
 
     class FakeCuda:
         Event = Ev
@@ -66,6 +72,14 @@ def test_no_collective_inside_timed_interval():
         @staticmethod
         def synchronize():
             log.append("sync")
+
+        @staticmethod
+        def current_stream():
+            return Stream()
+
+        @staticmethod
+        def stream(s):
+            return contextlib.nullcontext()
 
     class FakeTorch:
         cuda = FakeCuda
@@ -93,14 +107,20 @@ def test_no_collective_inside_timed_interval():
         def enable_timing(self, on):
             pass
 
-        def kernel_time(self, k):
-            return 0.0, 0
+        def kernel_spans(self, f, ev):
+            return []
 
-    class Wl:
-        graphs = {}
+    class Part:
+        def __init__(self):
+            self.eng, self.stream = Eng(), Stream()
 
         def step_fn(self, flags):
             return lambda: log.append("step")
+
+    class Wl:
+        def __init__(self):
+            self.parts = [Part(), Part()]
+            self.graphs = []
 
     real = bench.time.perf_counter
 
@@ -110,14 +130,15 @@ def test_no_collective_inside_timed_interval():
 
     bench.time.perf_counter = pc
     try:
-        (dev_s, host_s), _, _, _ = bench.measure(FakeTorch, FakeDist, 2, Eng(), Wl(), 0, "graph-k", 4, 1, 0.0,
-                                                 False)
+        (dev_s, host_s), _, _, _, _ = bench.measure(FakeTorch, FakeDist, 2, Wl(), 0, "graph-k", 4, 1, 0.0, False)
     finally:
         bench.time.perf_counter = real
     # the timed window: from the clock read followed by the opening event to the closing clock read
     i0 = max(i for i in range(len(log) - 1) if log[i] == "clock" and log[i + 1] == "event")
     i1 = max(i for i, v in enumerate(log) if v == "clock")
     window = log[i0:i1 + 1]
-    assert window == ["clock", "event", "replay", "event", "sync", "clock"], window
+    assert "barrier" not in window, window
+    assert window[:2] == ["clock", "event"] and window[-3:] == ["event", "sync", "clock"], window
+    assert window.count("replay") == 2   # one K-step graph per context
     assert "barrier" in log[:i0] and "barrier" in log[i1:]   # contract barriers, both outside
     assert dev_s == pytest.approx(1e-3)

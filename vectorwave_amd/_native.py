@@ -80,6 +80,8 @@ SIGNATURES = {
     "vw_ctx_enable_timing": (c_int, [c_void_p, c_int]),
     "vw_ctx_kernel_time": (c_int, [c_void_p, c_char_p, POINTER(c_double), POINTER(c_int64)]),
     "vw_ctx_reset_timing": (c_int, [c_void_p]),
+    "vw_ctx_kernel_spans": (c_int, [c_void_p, c_char_p, c_void_p, c_int64, POINTER(c_double), POINTER(c_double),
+                                    POINTER(c_int64)]),
     "vw_median_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_void_p, c_uint, c_void_p]),
     "vw_stddev_f64": (c_int, [c_void_p, c_void_p, c_int64, c_uint, c_void_p]),
     "vw_window_gather_abs_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_void_p, c_int64, c_int64]),

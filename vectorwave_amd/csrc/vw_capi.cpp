@@ -648,6 +648,33 @@ extern "C" vw_status vw_ctx_reset_timing(vw_ctx* c) {
   return ok();
 }
 
+// Start / end of the not-yet-collected timed launches of `family` (the last replay of each graph, or
+// the direct launches since the last collect), in ms after `ref_event` (a hipEvent_t recorded before
+// them, on any stream of the device) -- for callers that run several contexts concurrently and need
+// the wall window of a kernel family across them.  Call before vw_ctx_kernel_time, which consumes the
+// launches.  *count receives the number found (at most max are written).
+extern "C" vw_status vw_ctx_kernel_spans(vw_ctx* c, const char* family, void* ref_event, int64_t max,
+                                         double* start_ms, double* end_ms, int64_t* count) {
+  if (!c || !family || !ref_event || !count) return fail(VW_ERR_NULL, "null argument");
+  std::lock_guard<std::recursive_mutex> g(c->mu);
+  hipSetDevice(c->device);
+  int64_t n = 0;
+  for (const auto& tl : c->pending) {
+    if (tl.family != family) continue;
+    float a = 0.f, b = 0.f;
+    VW_HIP(hipEventSynchronize(tl.stop));
+    VW_HIP(hipEventElapsedTime(&a, (hipEvent_t)ref_event, tl.start));
+    VW_HIP(hipEventElapsedTime(&b, (hipEvent_t)ref_event, tl.stop));
+    if (n < max) {
+      if (start_ms) start_ms[n] = a;
+      if (end_ms) end_ms[n] = b;
+    }
+    ++n;
+  }
+  *count = n;
+  return ok();
+}
+
 extern "C" vw_status vw_ctx_kernel_time(vw_ctx* c, const char* family, double* total_ms, int64_t* launches) {
   if (!c || !family) return fail(VW_ERR_NULL, "null argument");
   std::lock_guard<std::recursive_mutex> g(c->mu);

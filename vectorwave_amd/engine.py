@@ -104,6 +104,16 @@ class Engine:
         _check(self.lib.vw_ctx_kernel_time(self.ctx, family.encode(), byref(ms), byref(n)))
         return ms.value, n.value
 
+    def kernel_spans(self, family: str, ref_event, max_n: int = 4096):
+        """[(start_ms, end_ms)] of the uncollected timed launches of `family`, relative to `ref_event`
+        (a torch.cuda.Event recorded before them); call before kernel_time (vw_ctx_kernel_spans)."""
+        st = (c_double * max_n)()
+        en = (c_double * max_n)()
+        n = c_int64()
+        _check(self.lib.vw_ctx_kernel_spans(self.ctx, family.encode(), c_void_p(ref_event.cuda_event), max_n, st, en,
+                                            byref(n)))
+        return [(st[i], en[i]) for i in range(min(n.value, max_n))]
+
     # -- array helpers ------------------------------------------------------------------------
     def _prep(self, x, dtype=None):
         """Returns (array, is_device, ptr, dtype_is_f32)."""
