@@ -475,44 +475,6 @@ def test_long_block_db8_j10(engine):
     exact(m2.detailPerLevel[:, 0, :], d)
 
 
-@pytest.mark.parametrize("opts", [dict(), dict(VW_COL_TK=500), dict(VW_COL_TK=1000, VW_COL_THREADS=256),
-                                  dict(VW_COL_C=2), dict(VW_COL_C=32), dict(VW_COL_C=16, VW_COL_THREADS=512),
-                                  dict(VW_COL_C=16, VW_COL_MIN=0), dict(VW_COL_MIN=0, VW_COL_TK=170)],
-                         ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()) or "default")
-def test_column_group_forward_bit_exact(engine, opts):
-    """Deep PERIODIC levels of the per-level path as one column-group launch each way (vw_device.h
-    k_forward_multi<COL> / k_inverse_col, vw_capi.cpp col_plan; opt-in VW_COL=1): residue blocks of C columns, several k-tiles with a
-    partial last one (TK=500: 1024 = 500 + 500 + 24), idle workgroups of the XCD-rounded grid, the
-    reach wrapping at both signal ends.  EXACT: bit-exact vs the restatement; FMA and fp32: identical
-    bits to the column sweeps (VW_COL=0: the same per-output operation sequence)."""
-    import torch
-    with engine.options(VW_FORCE_TILED=1, VW_COL=1, **opts):
-        for w, n, J in [(Daubechies.DB8, 1 << 15, 10), (H, 1 << 13, 12), (Daubechies.DB4, 1 << 14, 10)]:
-            x = signals(2, n, 31)
-            d, a = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, J, 0)   # BatchMODWT semantics
-            y = engine.inverse(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), w.wavelet_id, O.PERIODIC,
-                               J, 0)
-            for b in range(2):
-                d_ref, a_ref = O.decompose(x[b], *lohi(w), O.PERIODIC, J, core=False)
-                exact(d[:, b, :], d_ref)
-                exact(a[b], a_ref)
-                exact(y[b], O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(),
-                                          O.PERIODIC, w.wavelet_id))
-        for w, n, J, dt in [(Daubechies.DB8, 1 << 15, 10, torch.float64), (Coiflet.COIF5, 1 << 15, 8, torch.float32)]:
-            x = torch.empty((3, n), dtype=dt, device="cuda")
-            engine.fill_uniform(x, 8)
-            for flags in (0, nat.FLAG_FMA):
-                rl, rh = w.lowPassReconstruction(), w.highPassReconstruction()
-                d1, a1 = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, J, flags)
-                y1 = engine.inverse(d1, a1, rl, rh, w.wavelet_id, O.PERIODIC, J, flags)
-                with engine.options(VW_COL=0):
-                    d0, a0 = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, J, flags)
-                    y0 = engine.inverse(d1, a1, rl, rh, w.wavelet_id, O.PERIODIC, J, flags)
-                torch.cuda.synchronize()
-                assert torch.equal(d1, d0) and torch.equal(a1, a0), (w.name(), dt, flags)
-                assert torch.equal(y1, y0), (w.name(), dt, flags)
-
-
 # ---- device-resident path at the headline size --------------------------------------------------
 def test_headline_device_resident_properties(engine):
     import torch

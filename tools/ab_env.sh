@@ -11,15 +11,8 @@ for rep in ${REPS:-1}; do
 for v in "${VARS[@]}"; do
   name=${v%%:*}; envs=${v#*:}
   env ${LIB:+VW_LIB_PATH=$LIB} $envs timeout -k 10 120 python bench.py --no-cpu-baseline --no-alt ${BENCH_ARGS:-} > gpurun_out/ab_one.log 2>&1; rc=$?
-  python3 -c "
-import json,sys
-try:
-    d=json.loads([l for l in open('gpurun_out/ab_one.log') if l.startswith('{')][-1])
-    k=d['config'].get('kernels') or {}
-    print('$name', d['value'], d['ms_per_step'], ' '.join(f'{a}={b[\"ms_per_launch\"]}' for a,b in k.items()))
-except Exception as e:
-    print('$name', 'FAILED', open('gpurun_out/ab_one.log').read()[-600:])
-" | tee -a gpurun_out/ab_env.log
+  grep "^{" gpurun_out/ab_one.log | tail -1 > gpurun_out/ab_one.json; echo -n "$name " | tee -a gpurun_out/ab_env.log
+  python3 tools/bench_summary.py gpurun_out/ab_one.json | tee -a gpurun_out/ab_env.log || tail -c 600 gpurun_out/ab_one.log
   if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then echo "fatal rc=$rc"; exit $rc; fi
 done
 done

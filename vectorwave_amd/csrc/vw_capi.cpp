@@ -82,12 +82,7 @@ struct Tuning {
   int sweep_qc = kSweepChunk;  // VW_SWEEP_QC: q-chunk per sweep thread
   int unroll_max = kMaxTaps;   // VW_UNROLL_MAX: longest filter that runs the tap-unrolled fused kernels
   int blk = 10;                // VW_BLK: shortest filter that runs the register-blocked PERIODIC kernels (0 = off)
-  bool col = false;            // VW_COL=1: deep PERIODIC levels as one column group instead of column sweeps
                                // (measured on MI355X, db8 J=10 2^20 blocks: no faster than the sweeps yet)
-  int col_min = 100;           // VW_COL_MIN: smallest column tile, percent of the group's reach
-  int col_c = 0;               // VW_COL_C: residues per column block (0 = 64 bytes of samples)
-  int col_tk = 0;              // VW_COL_TK: decimated positions per column tile (0 = the most that fit LDS)
-  int col_threads = 1024;      // VW_COL_THREADS: workgroup size of the column-group forward
   bool deep = true;             // VW_DEEP=0|1: streaming deep-level forward (vw_deep.hip) off / on
   bool deep_inv = false;       // VW_DEEP_INV=1 (or VW_DEEP=1): the deep inverse too -- measured slower than
                                // the column sweeps on db8-stream (profiles/r03/ab_deep_db8_stream.log)
@@ -122,11 +117,6 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_SWEEP_QC") t.sweep_qc = v >= 16 ? v : d.sweep_qc;
   else if (k == "VW_UNROLL_MAX") t.unroll_max = v < 0 ? d.unroll_max : v;
   else if (k == "VW_BLK") t.blk = v < 0 ? d.blk : v;
-  else if (k == "VW_COL") t.col = v < 0 ? d.col : v != 0;
-  else if (k == "VW_COL_MIN") t.col_min = v < 0 ? d.col_min : v;
-  else if (k == "VW_COL_C") t.col_c = v < 0 ? d.col_c : v;
-  else if (k == "VW_COL_TK") t.col_tk = v < 0 ? d.col_tk : v;
-  else if (k == "VW_COL_THREADS") t.col_threads = (v == 256 || v == 512 || v == 1024) ? v : d.col_threads;
   else if (k == "VW_DEEP") { t.deep = v < 0 ? d.deep : v != 0; t.deep_inv = v < 0 ? d.deep_inv : v != 0; }
   else if (k == "VW_DEEP_INV") t.deep_inv = v < 0 ? d.deep_inv : v != 0;
   else if (k == "VW_DEEP_LDS") t.deep_lds = v <= 0 ? d.deep_lds : v;
@@ -142,7 +132,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
 static const char* const kTuningKeys[] = {
     "VW_NV", "VW_FWD_PERSIST", "VW_FWD_BUF", "VW_FORCE_TILED", "VW_FWD_REV", "VW_INV_REV",
     "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_MULTI_PF", "VW_NO_SWEEP", "VW_SWEEP_QC",
-    "VW_UNROLL_MAX", "VW_BLK", "VW_COL", "VW_COL_MIN", "VW_COL_C", "VW_COL_TK", "VW_COL_THREADS", "VW_FWD_NV",
+    "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV"};
 
 static Tuning read_tuning() {
@@ -834,48 +824,6 @@ static std::vector<int> level_groups(const Tuning& tu, const std::vector<LevelDe
   return g;
 }
 
-// Column group (vw_device.h k_forward_multi<COL>): the deep PERIODIC levels j..J of the per-level
-// path in one launch instead of one column sweep each.  Level j's spacing P = s_j divides N, so the
-// levels from j on only mix samples of one residue class mod P: a workgroup holds C consecutive
-// residues of a range of decimated positions (C samples = 64 bytes contiguous per position), the
-// levels' spacings become C, 2C, 4C, ... LDS positions, and the group's reach (sum (L-1) s_k / P
-// decimated positions, 465 at db8 levels 6-10) is re-read once per tile.
-struct ColPlan {
-  int g = 0, C = 0, tk = 0, ntk = 0, nb = 0, nk = 0, region = 0, threads = 0, lds = 0;
-  int ext[kMaxGroup + 1] = {};
-};
-
-static bool col_plan(const Tuning& tu, const std::vector<LevelDesc>& lv, int j, int J, int L, int V, int64_t N,
-                     int esz, bool ok, ColPlan* cp) {
-  if (!ok || !tu.col || !has_unrolled_taps(L)) return false;
-  const int P = lv[j - 1].s;
-  if (P < kSweepMinS || N % P != 0) return false;
-  const int g = std::min(J - j + 1, kMaxGroup);
-  if (g < 2) return false;
-  for (int k = 0; k < g; ++k)
-    if (lv[j - 1 + k].mode != kHaloPeriodic) return false;
-  const int C = tu.col_c ? tu.col_c : 64 / esz;
-  if (C % V != 0 || C > P || P % C != 0) return false;
-  ColPlan p;
-  p.g = g; p.C = C; p.nb = P / C; p.nk = (int)(N / P);
-  p.ext[g] = 0;
-  for (int k = g - 1; k >= 0; --k) p.ext[k] = p.ext[k + 1] + (int)round_up((int64_t)(L - 1) * C << k, V);
-  if (p.ext[0] / C >= p.nk) return false;
-  const int64_t room = (int64_t)kLdsBytes / esz / 2 - V - p.ext[0];  // two level buffers
-  int64_t tk = room / C;
-  if (tu.col_tk > 0) tk = std::min<int64_t>(tk, tu.col_tk);
-  tk = std::min<int64_t>(tk, p.nk);
-  // a tile narrower than the reach re-reads its input more than twice: the sweeps are better there
-  if (tk <= 0 || tk * C * 100 < (int64_t)p.ext[0] * tu.col_min) return false;
-  p.tk = (int)tk;
-  p.ntk = (int)round_up((p.nk + tk - 1) / tk, 8);
-  p.region = (int)round_up(p.ext[0] + tk * C + V, V);
-  p.lds = 2 * p.region * esz;
-  p.threads = tu.col_threads;
-  *cp = p;
-  return true;
-}
-
 // Streaming deep group (vw_deep.hip): PERIODIC levels jlo..jhi of the per-level path in one launch.
 // Needs level jlo's spacing P to divide N and hold C = 64 bytes of residues; every ring of the group
 // within the LDS budget.  Ring capacities: DMA-fed rings hold their history + two tiles (the next
@@ -1101,38 +1049,6 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
         j = je;
         continue;
       }
-      ColPlan cp;
-      if (groups[j - 1] == 1 && (lda % V) == 0 &&
-          col_plan(tu, lv, j, J, L, V, N, (int)sizeof(T), !validate && !hist, &cp)) {
-        const int je = j + cp.g - 1;
-        MultiArgs<T> m;
-        memset(&m, 0, sizeof(m));
-        m.src_a = src; m.lda = lda;
-        m.out_a = (je == J) ? approx : nxt;
-        bool al = aligned16(src) && aligned16(m.out_a);
-        for (int k = 0; k < cp.g; ++k) {
-          m.out_d[k] = details + (size_t)(j - 1 + k) * plane;
-          al = al && aligned16(m.out_d[k]);
-        }
-        if (al) {
-          for (int k = 0; k <= cp.g; ++k) m.ext[k] = cp.ext[k];
-          m.B = B; m.N = (int)N; m.tile = cp.tk * cp.C; m.nlev = cp.g; m.s0 = cp.C;
-          m.region = cp.region; m.vec_io = 1; m.taps = L;
-          m.col_c = cp.C; m.col_p = lv[j - 1].s; m.col_nb = cp.nb; m.col_nk = cp.nk; m.col_ntk = cp.ntk;
-          m.threads = cp.threads;
-          copy_taps(m.lo, lo, L);
-          copy_taps(m.hi, hi, L);
-          {
-            LaunchTimer lt(c, "forward_level");
-            hipError_t e = launch_forward_multi<T>(m, cp.lds, fma, c->stream);
-            if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward column group launch failed: %s", hipGetErrorString(e));
-          }
-          src = m.out_a;
-          lda = N;
-          j = je;
-          continue;
-        }
-      }
       if (groups[j - 1] >= 2) {
         const int g = groups[j - 1], je = j + g - 1;
         MultiArgs<T> m;
@@ -1353,21 +1269,6 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       for (int k = 0; k < groups[j - 1]; ++k) ext += round_up((int64_t)(L - 1) * lv[j - 1 + k].s, V);
       if ((mtile + ext) / V <= (int64_t)kMultiInvNI * 256) start_of[j + groups[j - 1] - 1] = j;
     }
-    // column group (k_inverse_col) over the deep levels jc..J: the forward's plan, taken only where it
-    // reaches level J and no multi-level tile group covers jc
-    int jc = 0;
-    ColPlan cp;
-    if (!pair && boundary == VW_PERIODIC) {
-      std::vector<char> in_multi(J + 1, 0);
-      for (int e = 1; e <= J; ++e)
-        for (int k = start_of[e]; start_of[e] > 0 && k <= e; ++k) in_multi[k] = 1;
-      for (int j = 1; j <= J && !jc; ++j) {
-        if (in_multi[j]) continue;
-        if (col_plan(tu, lv, j, J, L, V, N, (int)sizeof(T), true, &cp) && j + cp.g - 1 == J &&
-            (int64_t)cp.region / V <= (int64_t)kColNI * cp.threads)
-          jc = j;
-      }
-    }
     std::vector<char> in_group(J + 1, 0);  // levels inside a multi-level tile group
     for (int e = 1; e <= J; ++e)
       for (int k = start_of[e]; start_of[e] > 0 && k <= e; ++k) in_group[k] = 1;
@@ -1399,34 +1300,6 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         cur = d.out;
         j = jl;
         continue;
-      }
-      if (jc && j == J) {
-        MultiArgs<T> m;
-        memset(&m, 0, sizeof(m));
-        m.src_a = cur;
-        m.out_a = (jc == 1) ? y : nxt;
-        bool al = aligned16(cur) && aligned16(m.out_a);
-        for (int k = 0; k < cp.g; ++k) {
-          const LevelDesc& d = lv[jc - 1 + k];
-          m.src_d[k] = d.use_d ? details + (size_t)(jc - 1 + k) * plane : nullptr;
-          m.thr[k] = thr ? thr + (size_t)(jc - 1 + k) * (size_t)thr_ld : nullptr;
-          al = al && aligned16(m.src_d[k]);
-          m.ext[k] = (k > 0 ? m.ext[k - 1] : 0) + (int)round_up((int64_t)(L - 1) * cp.C << k, V);
-        }
-        if (al) {
-          m.B = B; m.N = (int)N; m.tile = cp.tk * cp.C; m.nlev = cp.g; m.s0 = cp.C;
-          m.region = cp.region; m.vec_io = 1; m.soft = soft; m.taps = L;
-          m.col_c = cp.C; m.col_p = lv[jc - 1].s; m.col_nb = cp.nb; m.col_nk = cp.nk; m.col_ntk = cp.ntk;
-          m.threads = cp.threads;
-          copy_taps(m.lo, lo, L);
-          copy_taps(m.hi, hi, L);
-          LaunchTimer lt(c, "inverse_level");
-          hipError_t e = launch_inverse_multi<T>(m, cp.lds, fma, c->stream);
-          if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse column group launch failed: %s", hipGetErrorString(e));
-          cur = m.out_a;
-          j = jc;
-          continue;
-        }
       }
       if (start_of[j] > 0) {
         const int j0 = start_of[j], g = j - j0 + 1;

@@ -378,6 +378,9 @@ __device__ __forceinline__ void for_vecs(int nvec, F&& fn) {
 #ifndef VW_FWD_STORE_AUX
 #define VW_FWD_STORE_AUX VW_STORE_AUX  // forward coefficient rows (read next by an inverse)
 #endif
+#ifndef VW_BLK_NT_M
+#define VW_BLK_NT_M 8  // k_forward_blk: vector strides m below this store write-back (see there)
+#endif
 #ifndef VW_INV_STORE_AUX
 #define VW_INV_STORE_AUX VW_STORE_AUX  // inverse output rows
 #endif
@@ -1197,10 +1200,21 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
     if (m) {
       vb = blk_base<NV>(m);
       blk_fwd<T, L, FMA, NV>(X, blk_layout(m, NV, p.blk_tight), HLV, vb, m, flo, fhi, al, ah);
+      if (m < VW_BLK_NT_M) {
+        // a lane's outputs are m*16-byte pieces NV*m*16 bytes apart: write-back stores, so that L2
+        // merges a line's pieces before it goes to HBM (nontemporal stores of 16-byte pieces wrote
+        // 1.5x the algorithmic bytes on coif5 fp32, profiles/hbm_traffic_coif5-f32.json)
 #pragma unroll
-      for (int r = 0; r < NV; ++r) {
-        store_vec<VW_FWD_STORE_AUX>(dout, (vb + r * m) * V, N, true, ah[r]);
-        if (last) store_vec<VW_FWD_STORE_AUX>(aout, (vb + r * m) * V, N, true, al[r]);
+        for (int r = 0; r < NV; ++r) {
+          store_vec<0>(dout, (vb + r * m) * V, N, true, ah[r]);
+          if (last) store_vec<0>(aout, (vb + r * m) * V, N, true, al[r]);
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < NV; ++r) {
+          store_vec<VW_FWD_STORE_AUX>(dout, (vb + r * m) * V, N, true, ah[r]);
+          if (last) store_vec<VW_FWD_STORE_AUX>(aout, (vb + r * m) * V, N, true, al[r]);
+        }
       }
     } else {
       // s < V (m == 0): only the register-window forms.  (fwd_row's strided form, unreachable here,
@@ -1626,40 +1640,8 @@ __global__ void __launch_bounds__(256) k_inverse_sweep(const LevelArgs<T> p) {
 // (ScalarOps.java:700-723 reads t - l*s), to the right in the inverse (MultiLevelMODWTTransform
 // .java:576-589 reads t + l*s).  The redundant ext/tile of the arithmetic buys one HBM round trip
 // per group instead of one per level.
-// Column layout (MultiArgs col_*): workgroup -> (k-tile, column block).  The column blocks of one
-// k-tile share HBM lines (a block holds col_c residues, a line more), so they are dispatched to the
-// same XCD (workgroup i runs on XCD i mod 8) back to back: grid.x = col_ntk * col_nb with col_ntk a
-// multiple of 8, and a k-tile's blocks sit 8 apart in blockIdx.x.
-struct ColTile {
-  int k0, r0, cnt;  // first decimated position, first residue, stored LDS positions (multiple of col_c)
-  bool ok;
-};
-template <typename T>
-__device__ __forceinline__ ColTile col_tile(const MultiArgs<T>& p) {
-  const int bx = blockIdx.x, xcd = bx & 7, slot = bx >> 3;
-  const int kt = (slot / p.col_nb) * 8 + xcd, cb = slot % p.col_nb;
-  const int tk = p.tile / p.col_c;
-  ColTile t;
-  t.k0 = kt * tk;
-  t.r0 = cb * p.col_c;
-  t.ok = t.k0 < p.col_nk;
-  t.cnt = t.ok ? min(tk, p.col_nk - t.k0) * p.col_c : 0;
-  return t;
-}
-// Sample index of LDS position q >= lo (lo = -ext, a multiple of col_c), decimated positions wrapped
-// once (host contract: ext / col_c < col_nk).
-template <typename T>
-__device__ __forceinline__ long long col_pos(const MultiArgs<T>& p, const ColTile& t, int q) {
-  const int c = p.col_c;
-  const int qq = q + 4 * p.col_nk * c;  // >= 0 (ext < nk * c)
-  int kk = t.k0 + qq / c - 4 * p.col_nk;
-  if (kk < 0) kk += p.col_nk;
-  else if (kk >= p.col_nk) kk -= p.col_nk;
-  return (long long)kk * p.col_p + t.r0 + (qq % c);
-}
-
-template <typename T, int L, bool FMA, bool COL>
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, COL ? 1024 : 256))) k_forward_multi(const MultiArgs<T> p) {
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(256) k_forward_multi(const MultiArgs<T> p) {
   constexpr int V = VT<T>::V;
   using vec = typename VT<T>::v;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1667,23 +1649,11 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, COL ? 1024 : 256))
   T* Y = X + p.region;
   const long long b = blockIdx.y;
   const int N = p.N;
-  int ts = 0, cnt, span;
-  ColTile ct{};
-  if constexpr (COL) {
-    ct = col_tile(p);
-    if (!ct.ok) return;
-    cnt = span = ct.cnt;
-    // host contract: vector io (16-B aligned rows, P and col_c multiples of V)
-    const T* src = p.src_a + b * p.lda;
-    for (int q = -p.ext[0] + (int)threadIdx.x * V; q < span; q += blockDim.x * V)
-      *reinterpret_cast<vec*>(X + q) = __builtin_nontemporal_load(reinterpret_cast<const vec*>(src + col_pos(p, ct, q)));
-  } else {
-    ts = blockIdx.x * p.tile;
-    cnt = min(p.tile, N - ts);
-    span = (cnt + V - 1) / V * V;
-    tile_to_lds(X, p.src_a + b * p.lda, N, ts, -p.ext[0], span, kHaloPeriodic, 0, (const T*)nullptr, 0,
-                (const T*)nullptr, T(0), 0, false, p.vec_io != 0);
-  }
+  const int ts = blockIdx.x * p.tile;
+  const int cnt = min(p.tile, N - ts);
+  const int span = (cnt + V - 1) / V * V;
+  tile_to_lds(X, p.src_a + b * p.lda, N, ts, -p.ext[0], span, kHaloPeriodic, 0, (const T*)nullptr, 0,
+              (const T*)nullptr, T(0), 0, false, p.vec_io != 0);
   const bool vec_ok = p.vec_io != 0;
   for (int k = 0; k < p.nlev; ++k) {
     lds_barrier();  // X complete; every read of Y (the previous level's input) done
@@ -1693,59 +1663,6 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, COL ? 1024 : 256))
     const bool last = k == p.nlev - 1;
     T* od = p.out_d[k] + b * (size_t)N + ts;
     T* oa = p.out_a + b * (size_t)N + ts;
-    if constexpr (COL && L > 0) {
-      // Register-blocked taps (column layout: s is a multiple of V): a thread owns the outputs
-      // vb, vb+m, .., vb+(NI-1)m (vectors, m = s/V), which read the same LDS vectors shifted by one
-      // tap -- NI+L-1 reads per thread instead of NI*L.  The window runs j downwards so each output
-      // still sums its taps i = r - j ascending (ScalarOps.java:700-723 order): bit-identical.
-      constexpr int NI = kColRB;
-      const int m = s / V;
-      const int vlo = q_lo / V;
-      const int lim = span / V - 1;  // last vector of X (reads past it feed only unstored outputs)
-      const int pairs = (nv + m * NI - 1) / (m * NI) * m;
-      for (int pr = threadIdx.x; pr < pairs; pr += blockDim.x) {
-        const int vb = (pr / m) * m * NI + pr % m;
-        T al[NI][V], ah[NI][V];
-#pragma unroll
-        for (int r = 0; r < NI; ++r)
-#pragma unroll
-          for (int e = 0; e < V; ++e) { al[r][e] = T(0); ah[r][e] = T(0); }
-#pragma unroll
-        for (int j = NI - 1; j >= -(L - 1); --j) {
-          const vec x = *reinterpret_cast<const vec*>(X + min(vlo + vb + j * m, lim) * V);
-#pragma unroll
-          for (int r = 0; r < NI; ++r) {
-            const int i = r - j;
-            if (i >= 0 && i < L)
-#pragma unroll
-              for (int e = 0; e < V; ++e) {
-                al[r][e] = madd<FMA>(al[r][e], x[e], p.lo[i]);
-                ah[r][e] = madd<FMA>(ah[r][e], x[e], p.hi[i]);
-              }
-          }
-        }
-#pragma unroll
-        for (int r = 0; r < NI; ++r) {
-          const int w = vb + r * m;
-          if (w < nv) {
-            const int q0 = q_lo + w * V;
-            if (q0 >= 0) {
-              const int g = (int)col_pos(p, ct, q0);
-              store_vec(od, g, N, true, ah[r]);
-              if (last) store_vec(oa, g, N, true, al[r]);
-            }
-            if (!last) {
-              vec o;
-#pragma unroll
-              for (int e = 0; e < V; ++e) o[e] = al[r][e];
-              *reinterpret_cast<vec*>(Y + q0) = o;
-            }
-          }
-        }
-      }
-      T* t = X; X = Y; Y = t;
-      continue;
-    }
     for (int w = threadIdx.x; w < nv; w += blockDim.x) {
       const int q0 = q_lo + w * V;
       T al[V], ah[V];
@@ -1753,14 +1670,8 @@ __global__ void __attribute__((amdgpu_flat_work_group_size(1, COL ? 1024 : 256))
       for (int e = 0; e < V; ++e) { al[e] = T(0); ah[e] = T(0); }
       fwd_vec<T, L, FMA>(X, q0, s, p.lo, p.hi, p.taps, al, ah);
       if (q0 >= 0) {  // the tile's own outputs (vectors never straddle 0: q_lo is a multiple of V)
-        if constexpr (COL) {
-          const int g = (int)col_pos(p, ct, q0);
-          store_vec(od, g, N, true, ah);
-          if (last) store_vec(oa, g, N, true, al);
-        } else {
-          store_vec(od, q0, cnt, vec_ok, ah);
-          if (last) store_vec(oa, q0, cnt, vec_ok, al);
-        }
+        store_vec(od, q0, cnt, vec_ok, ah);
+        if (last) store_vec(oa, q0, cnt, vec_ok, al);
       }
       if (!last) {
         vec o;
@@ -1927,134 +1838,6 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
       }
     }
     if (pf) d_store(k - 1);
-  }
-}
-
-// Inverse column group (the deep PERIODIC levels, MultiArgs col_*; host: vw_capi.cpp col_plan): the
-// layout of k_forward_multi<COL>, levels top..0 of the group.  A = a_k over [0, span + ext[k]) (right
-// reach, MultiLevelMODWTTransform.java:576-589 reads t + l*s), D = d_k (thresholded on load for
-// denoise); a_{k-1} goes to registers (kColNI vectors per thread, host contract) and over A after a
-// barrier.  Sums: all approximation taps, then all detail taps (K4), bit-identical to the sweeps.
-template <typename T>
-__device__ __forceinline__ void col_load(const MultiArgs<T>& p, const ColTile& ct, T* buf, const T* src, int hi_q,
-                                         const T* th, int soft) {
-  constexpr int V = VT<T>::V;
-  using vec = typename VT<T>::v;
-  const T thb = th ? th[blockIdx.y] : T(0);
-  for (int q = (int)threadIdx.x * V; q < hi_q; q += blockDim.x * V) {
-    vec v;
-    if (src) {
-      v = __builtin_nontemporal_load(reinterpret_cast<const vec*>(src + col_pos(p, ct, q)));
-      if (th)
-#pragma unroll
-        for (int e = 0; e < V; ++e) v[e] = threshold_t(v[e], thb, soft);
-    } else {
-#pragma unroll
-      for (int e = 0; e < V; ++e) v[e] = T(0);
-    }
-    *reinterpret_cast<vec*>(buf + q) = v;
-  }
-}
-
-template <typename T, int L, bool FMA>
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, 1024))) k_inverse_col(const MultiArgs<T> p) {
-  constexpr int V = VT<T>::V;
-  constexpr int NI = kColNI;
-  using vec = typename VT<T>::v;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  T* const A = reinterpret_cast<T*>(smem);
-  T* const D = A + p.region;
-  const ColTile ct = col_tile(p);
-  if (!ct.ok) return;
-  const long long b = blockIdx.y;
-  const size_t row = (size_t)b * (size_t)p.N;
-  const int span = ct.cnt;
-  const int top = p.nlev - 1;
-  col_load(p, ct, A, p.src_a ? p.src_a + row : nullptr, span + p.ext[top], (const T*)nullptr, 0);
-  for (int k = top; k >= 0; --k) {
-    col_load(p, ct, D, p.src_d[k] ? p.src_d[k] + row : nullptr, span + p.ext[k], p.thr[k], p.soft);
-    lds_barrier();  // A and D complete
-    const int s = p.s0 << k;
-    const int nv = (span + (k > 0 ? p.ext[k - 1] : 0)) / V;  // the tile + what the next levels read
-    if constexpr (L > 0) {
-      // register-blocked taps, one (block, column) pair per thread: as k_inverse_multi (window j = r + i
-      // ascending: taps i ascending per output, approximation branch then detail branch)
-      constexpr int RB = kColRB;
-      const int m = s / V;
-      const int pairs = (nv + m * RB - 1) / (m * RB) * m;
-      if (pairs <= (int)blockDim.x) {
-        const int pr = threadIdx.x;
-        const int vb = (pr / m) * m * RB + pr % m;
-        const int lim = (span + p.ext[k]) / V - 1;  // last vector of the A/D regions
-        T ar[RB][V];
-#pragma unroll
-        for (int r = 0; r < RB; ++r)
-#pragma unroll
-          for (int e = 0; e < V; ++e) ar[r][e] = T(0);
-        if (pr < pairs) {
-#pragma unroll
-          for (int br = 0; br < 2; ++br) {
-            const T* buf = br == 0 ? A : D;
-            const T* f = br == 0 ? p.lo : p.hi;
-#pragma unroll
-            for (int j = 0; j < RB + L - 1; ++j) {
-              const vec x = *reinterpret_cast<const vec*>(buf + min(vb + m * j, lim) * V);
-#pragma unroll
-              for (int r = 0; r < RB; ++r) {
-                const int i = j - r;
-                if (i >= 0 && i < L)
-#pragma unroll
-                  for (int e = 0; e < V; ++e) ar[r][e] = madd<FMA>(ar[r][e], x[e], f[i]);
-              }
-            }
-          }
-          if (k == 0) {
-#pragma unroll
-            for (int r = 0; r < RB; ++r)
-              if (vb + m * r < nv) store_vec(p.out_a + row, (int)col_pos(p, ct, (vb + m * r) * V), p.N, true, ar[r]);
-          }
-        }
-        if (k == 0) break;
-        lds_barrier();  // every read of A and D done
-        if (pr < pairs) {
-#pragma unroll
-          for (int r = 0; r < RB; ++r) {
-            if (vb + m * r < nv) {
-              vec o;
-#pragma unroll
-              for (int e = 0; e < V; ++e) o[e] = ar[r][e];
-              *reinterpret_cast<vec*>(A + (vb + m * r) * V) = o;
-            }
-          }
-        }
-        continue;
-      }
-    }
-    T acc[NI][V];
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int w = threadIdx.x + i * blockDim.x;
-#pragma unroll
-      for (int e = 0; e < V; ++e) acc[i][e] = T(0);
-      if (w < nv) {
-        inv_branch<T, L, FMA>(A, w * V, s, 1, 0, p.lo, p.taps, acc[i]);
-        inv_branch<T, L, FMA>(D, w * V, s, 1, 0, p.hi, p.taps, acc[i]);
-        if (k == 0) store_vec(p.out_a + row, (int)col_pos(p, ct, w * V), p.N, true, acc[i]);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // one vector's LDS reads in flight at a time (VGPR budget)
-    }
-    if (k == 0) break;
-    lds_barrier();  // every read of A and D done
-#pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int w = threadIdx.x + i * blockDim.x;
-      if (w < nv) {
-        vec o;
-#pragma unroll
-        for (int e = 0; e < V; ++e) o[e] = acc[i][e];
-        *reinterpret_cast<vec*>(A + w * V) = o;
-      }
-    }
   }
 }
 

@@ -128,8 +128,6 @@ struct LevelArgs {
 // launch, the intermediate approximations kept in LDS (vw_device.h k_forward_multi / k_inverse_multi).
 constexpr int kMaxGroup = 8;
 constexpr int kMultiInvNI = 8;  // k_inverse_multi: output vectors per thread (256 threads)
-constexpr int kColNI = 12;     // k_inverse_col: output vectors per thread (host contract: region / V <= kColNI * threads)
-constexpr int kColRB = 8;      // column-group kernels: register-blocked outputs per thread
 constexpr int kMultiPF = 6;     // k_inverse_multi: prefetched detail vectors per thread (256 threads)
 template <typename T>
 struct MultiArgs {
@@ -153,17 +151,6 @@ struct MultiArgs {
   int taps;
   int rblk;                  // inverse: register-blocked taps where S is a multiple of V
   int pf;                    // inverse: next level's detail tile prefetched into registers
-  // Column layout (deep PERIODIC levels, vw_device.h col_pos): col_c = 0 is the natural layout.
-  // Otherwise the group's first level has spacing P = col_p, which divides N; every level of the
-  // group then only mixes samples of one residue class mod P.  A workgroup holds col_c consecutive
-  // residues [r0, r0 + col_c) of a range of decimated positions k (sample k*P + r): LDS position
-  // q = kk*col_c + c, so all spacings (s0, ext, tile) are in LDS units, s0 = col_c.
-  int col_c;
-  int col_p;
-  int col_nb;                // column blocks per k-tile (P / col_c)
-  int col_nk;                // decimated length N / P
-  int col_ntk;               // k-tiles per signal, rounded up to a multiple of 8 (XCD-aware grid)
-  int threads;               // workgroup size of the launch
   T lo[kMaxTaps];
   T hi[kMaxTaps];
 };
