@@ -46,6 +46,11 @@ ACC_NAME = {
     False: "exact (separate multiply and add in the reference's tap order; bit-identical to vectorwave-core)",
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
+# Vector-ALU peaks for the FMA work of the taps: fp32 from the microarchitecture guide (157.3 TFLOP/s
+# vector), fp64 the MI355X spec sheet's 78.6 (the guide lists no fp64 figure); beside them the issue
+# rates tools/valubench.hip measured on this GPU (profiles/r03/valubench.log)
+VALU_PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}
+VALU_MEASURED_TFLOPS = {"f32": {"v_fma_f32": 95.3, "v_pk_fma_f32": 117.4}, "f64": {"v_fma_f64": 61.6}}
 COPY_GBS = 6167.2      # measured plain-copy kernel ("copy 1->1 nt", profiles/r01/membench_v2.log)
 
 LAUNCH_DESC = {
@@ -576,6 +581,10 @@ def run(args, world, rank, local):
         del wk1
     kkernels = {k: {"launches_per_step": round(n / max(ksampled, 1), 3), "ms_per_launch": round(ms / n, 5)}
                 for k, (ms, n) in kfams.items()}
+    # algorithmic flops per pass: every level applies both filters, L taps each, one FMA (2 flop) per
+    # tap and sample (ScalarOps.java:700-723, MultiLevelMODWTTransform.java:576-589)
+    L = len(w.lowPassDecomposition())
+    pass_flop = {"forward": 4 * L * J * units, "inverse": 4 * L * J * units, "sigma": 0}
     roof = None
     if kpass_ms:
         dom = max(kpass_ms, key=lambda f: kpass_ms[f])
@@ -598,6 +607,22 @@ def run(args, world, rank, local):
                 "step": {"bytes": step_bytes, "ms": round(elapsed / args.steps * 1e3, 5),
                          "achieved": round(step_bytes / (elapsed / args.steps) / 1e9, 1),
                          "frac": round(step_bytes / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)}}
+        # the compute roof of the same pass: which floor (bytes at the HBM peak, flops at the VALU peak)
+        # is higher decides the bound; long filters (coif5, L = 30) are VALU-bound, db4 is HBM-bound
+        tflops = pass_flop[dom] / (kpass_ms[dom] * 1e-3) / 1e12
+        vpk = VALU_PEAK_TFLOPS[dtype]
+        hbm_floor = pass_bytes[dom] / (HBM_PEAK_GBS * 1e9) * 1e3
+        valu_floor = pass_flop[dom] / (vpk * 1e12) * 1e3
+        compute = {"flop_per_launch": pass_flop[dom], "achieved": round(tflops, 2), "peak": vpk, "unit": "TFLOP/s",
+                   "frac": round(tflops / vpk, 4), "measured_issue_TFLOPs": VALU_MEASURED_TFLOPS[dtype],
+                   "floor_ms": {"hbm": round(hbm_floor, 5), "valu": round(valu_floor, 5)}}
+        roof["compute"] = compute
+        if valu_floor > hbm_floor:
+            # VALU-bound pass: the headline roofline fields carry the compute roof; the HBM figures stay
+            # beside them
+            roof["hbm"] = {k: roof[k] for k in ("achieved", "peak", "unit", "frac")}
+            roof.update({"bound": "valu", "achieved": compute["achieved"], "peak": vpk, "unit": "TFLOP/s",
+                         "frac": compute["frac"]})
 
     # ---- the other accumulation mode, same rows, timed the same way (beside the headline)
     alt = None

@@ -47,17 +47,22 @@ __device__ __forceinline__ T madd(T acc, T x, T f) {
   else return acc + x * f;
 }
 
-// acc_e (+)= x_e * f over one 16-byte vector of outputs, per element.  VW_PK_F32=1 (experiment builds):
-// fp32 as two packed operations per pair (v_pk_fma_f32; EXACT v_pk_mul_f32 + v_pk_add_f32, the same
-// rounding per element).  Measured on coif5 fp32 (profiles/r03/ab_pk_f32.log): the blocked forward
-// 7.40 -> 8.08 ms, the inverse unchanged, with 34 % fewer VALU instructions -- these kernels are not
-// VALU-issue-bound, so the default stays per element.
+// acc_e (+)= x_e * f over one 16-byte vector of outputs, per element.  PK (fp32 only): two packed
+// operations per pair (v_pk_fma_f32; EXACT v_pk_mul_f32 + v_pk_add_f32, the same rounding per
+// element).  Measured on coif5 fp32, same box (profiles/r03/ab_coif5_pk_cinv.log): packed forward
+// 6.46 -> 5.88 ms; packed inverse 7.05 -> 7.23 ms.  So the forward kernels pack (VW_PK_F32_FWD,
+// default 1) and the inverse ones do not (VW_PK_F32, default 0).  tools/valubench.hip: v_fma_f32
+// issues 95 TFLOP/s, v_pk_fma_f32 117 on this GPU.
 #ifndef VW_PK_F32
 #define VW_PK_F32 0
 #endif
-template <bool FMA, typename T, typename X>
+#ifndef VW_PK_F32_FWD
+#define VW_PK_F32_FWD 1
+#endif
+constexpr bool kPkFwd = VW_PK_F32_FWD != 0;
+template <bool FMA, bool PK = (VW_PK_F32 != 0), typename T, typename X>
 __device__ __forceinline__ void vmadd(T* acc, const X& x, T f) {
-  if constexpr (VW_PK_F32 && std::is_same<T, float>::value) {
+  if constexpr (PK && std::is_same<T, float>::value) {
     typedef float f2 __attribute__((ext_vector_type(2)));
     const f2 fv = {f, f};
 #pragma unroll
@@ -189,8 +194,8 @@ __device__ __forceinline__ void fwd_window(const T* buf, int t0, const T* lo, co
     for (int i = I0; i < I1; ++i) { fl[i - I0] = lo[i]; fh[i - I0] = hi[i]; }
 #pragma unroll
     for (int i = I0; i < I1; ++i) {
-      vmadd<FMA>(al, &w[-i * S - A], fl[i - I0]);
-      vmadd<FMA>(ah, &w[-i * S - A], fh[i - I0]);
+      vmadd<FMA, kPkFwd>(al, &w[-i * S - A], fl[i - I0]);
+      vmadd<FMA, kPkFwd>(ah, &w[-i * S - A], fh[i - I0]);
     }
   });
 }
@@ -208,8 +213,8 @@ __device__ __forceinline__ void fwd_vec(const T* buf, int t0, int S, const T* lo
 #pragma unroll
     for (int i = 0; i < L; ++i) {   // S is a multiple of V: aligned 16-byte reads
       const vec v = *reinterpret_cast<const vec*>(buf + t0 - i * S);
-      vmadd<FMA>(al, v, lo[i]);
-      vmadd<FMA>(ah, v, hi[i]);
+      vmadd<FMA, kPkFwd>(al, v, lo[i]);
+      vmadd<FMA, kPkFwd>(ah, v, hi[i]);
     }
   } else {
     for (int i = 0; i < taps; ++i) {
@@ -592,8 +597,8 @@ __device__ __forceinline__ void fwd_row_t(const T* buf, int nvec, int s, const T
 #pragma unroll
       for (int i = 0; i < L; ++i) {  // s is a multiple of V: aligned 16-byte reads
         const vec v = *reinterpret_cast<const vec*>(buf + t0 - i * s);
-        vmadd<FMA>(al, v, lo[i]);
-        vmadd<FMA>(ah, v, hi[i]);
+        vmadd<FMA, kPkFwd>(al, v, lo[i]);
+        vmadd<FMA, kPkFwd>(ah, v, hi[i]);
         if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // <= 4 reads in flight (VGPR budget)
       }
     } else {
@@ -1099,6 +1104,81 @@ __device__ __forceinline__ void blk_inv_branch(const T* R, const BlkLayout& lo, 
     for (int e = 0; e < V; ++e) asm volatile("" : "+v"(acc[r][e]));  // pin the sums (see inv_row_t)
 }
 
+// Compile-time form of blk_layout at vector stride M (NV outputs per column, TIGHT: blk_tight).  A
+// thread's block base vb = (tid/M)*M*NV + tid%M; when M*NV is a multiple of the pad group 2^SH, the
+// physical offset of logical vector vb + q*M from vb's is off(q) for every thread, so the branch
+// reads at immediate offsets from one base address instead of computing u + (u >> SH)*PAD per read.
+template <int M, int NV, int TIGHT>
+struct BlkC {
+  static constexpr int SH = (M >= 16) ? 30 : (NV >= 8 ? (TIGHT ? 4 : 3) : (M == 8 ? 3 : 2));
+  static constexpr int PAD = (M >= 16) ? 0 : (NV >= 8 ? 1 : (M == 8 ? 2 : 1));
+  static constexpr bool ok = PAD == 0 || (M * NV) % (1 << SH) == 0;
+  static constexpr int off(int q) { return q * M + ((q * M) >> SH) * PAD; }
+};
+
+// blk_inv_branch at a compile-time stride: Rb = R + blk_phys(layout, vb) * V
+template <typename T, int L, bool FMA, int NV, int M, int TIGHT>
+__device__ __forceinline__ void blk_inv_branch_c(const T* Rb, const T* f, T (&acc)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  using C = BlkC<M, NV, TIGHT>;
+  constexpr int TC = blk_chunk<T, NV>();
+  static_for<0, (L + TC - 1) / TC>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * TC;
+    constexpr int I1 = (I0 + TC < L) ? I0 + TC : L;
+    T fc[I1 - I0];
+#pragma unroll
+    for (int i = I0; i < I1; ++i) fc[i - I0] = f[i];
+#pragma unroll
+    for (int q = I0; q < I1 + NV - 1; ++q) {
+      const vec x = *reinterpret_cast<const vec*>(Rb + C::off(q) * V);
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        const int i = q - r;
+        if (i >= I0 && i < I1) {
+          vmadd<FMA>(acc[r], x, fc[i - I0]);
+        }
+      }
+      if (((q - I0) & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+#pragma unroll
+  for (int r = 0; r < NV; ++r)
+#pragma unroll
+    for (int e = 0; e < V; ++e) asm volatile("" : "+v"(acc[r][e]));
+}
+
+// One inverse branch at vector stride m >= 1: the compile-time forms for m = 1..64 (immediate LDS
+// offsets stay below 64 KiB for L <= 30), the generic one otherwise.  Same reads, same sums.
+template <typename T, int L, bool FMA, int NV>
+__device__ __forceinline__ void blk_inv_any(const T* R, const BlkLayout& lo, int tight, int vb, int m, const T* f,
+                                            T (&acc)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  if constexpr (NV >= 8) {
+    // measured slower at NV = 8 (sym8 fp64 inverse 7.18 -> 8.08 ms, profiles/r03/ab_sym8_cinv.log)
+    blk_inv_branch<T, L, FMA, NV>(R, lo, vb, m, f, acc);
+  } else {
+    const T* Rb = R + blk_phys(lo, vb) * V;
+    auto go = [&](auto mc, auto tc) __attribute__((always_inline)) {
+      constexpr int M = decltype(mc)::value, TT = decltype(tc)::value;
+      if constexpr (BlkC<M, NV, TT>::ok) blk_inv_branch_c<T, L, FMA, NV, M, TT>(Rb, f, acc);
+      else blk_inv_branch<T, L, FMA, NV>(R, lo, vb, m, f, acc);
+    };
+    auto go_m = [&](auto mc) __attribute__((always_inline)) { go(mc, std::integral_constant<int, 0>{}); };
+    (void)tight;  // the tight layout exists only at NV >= 8
+    switch (m) {
+      case 1: go_m(std::integral_constant<int, 1>{}); break;
+      case 2: go_m(std::integral_constant<int, 2>{}); break;
+      case 4: go_m(std::integral_constant<int, 4>{}); break;
+      case 8: go_m(std::integral_constant<int, 8>{}); break;
+      case 16: go_m(std::integral_constant<int, 16>{}); break;
+      case 32: go_m(std::integral_constant<int, 32>{}); break;
+      case 64: go_m(std::integral_constant<int, 64>{}); break;
+      default: blk_inv_branch<T, L, FMA, NV>(R, lo, vb, m, f, acc); break;
+    }
+  }
+}
+
 // The forward (reads t - i*s, both filters from one set of reads): within a tap chunk q runs down so
 // that for every output r the tap i = r - q ascends; chunks ascend.  Input vector u sits at logical
 // u + HLV.
@@ -1125,8 +1205,8 @@ __device__ __forceinline__ void blk_fwd(const T* X, const BlkLayout& lo, int HLV
       for (int r = 0; r < NV; ++r) {
         const int i = r - q;
         if (i >= I0 && i < I1) {
-          vmadd<FMA>(al[r], x, fl[i - I0]);
-          vmadd<FMA>(ah[r], x, fh[i - I0]);
+          vmadd<FMA, kPkFwd>(al[r], x, fl[i - I0]);
+          vmadd<FMA, kPkFwd>(ah[r], x, fh[i - I0]);
         }
       }
       if (((NV - 1 - I0 - q) & 3) == 3) __builtin_amdgcn_sched_barrier(0);
@@ -1309,7 +1389,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_blk(const InvArg
     const int vb = m ? blk_base<NV>(m) : 0;
     lds_barrier();  // R = a_j + wrap images
     zero_regs<T, NV>(acc);
-    if (m) blk_inv_branch<T, L, FMA, NV>(R, lo, vb, m, flo, acc);
+    if (m) blk_inv_any<T, L, FMA, NV>(R, lo, p.blk_tight, vb, m, flo, acc);
     else inv_row<T, L, FMA, NV>(R, nvec, lv.s, 1, 0, flo, p.taps, acc);
     lds_barrier();  // every approximation-branch read done
     wait_vmem();    // the d_j prefetch
@@ -1318,7 +1398,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_blk(const InvArg
       load_row_regs<T, NV>(dreg, p.details + (size_t)(j - 2) * plane + b * (size_t)N, N, nvec, true,
                            p.lv[j - 2].use_d == 0);
     lds_barrier();  // R = d_j + wrap images
-    if (m) blk_inv_branch<T, L, FMA, NV>(R, lo, vb, m, fhi, acc);
+    if (m) blk_inv_any<T, L, FMA, NV>(R, lo, p.blk_tight, vb, m, fhi, acc);
     else inv_row<T, L, FMA, NV>(R, nvec, lv.s, 1, 0, fhi, p.taps, acc);
     if (j > 1) {
       lds_barrier();  // every detail-branch read done
