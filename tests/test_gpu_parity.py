@@ -434,6 +434,36 @@ def test_multilevel_tiles_bit_exact(engine, tile):
             exact(y[b], y_ref)
 
 
+@pytest.mark.parametrize("opts", [dict(VW_MULTI_PAD=0), dict(VW_MULTI_INV_TILE=1792), dict(VW_MULTI_INV_TILE=1024),
+                                  dict(VW_MULTI_INV_TILE=512, VW_MULTI_TILE=512)],
+                         ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
+def test_multilevel_inverse_padded_layout(engine, opts):
+    """k_inverse_multi's padded LDS layout at the register-blocked levels (VW_MULTI_PAD, default on) and
+    its own tile (VW_MULTI_INV_TILE): EXACT bit-exact vs the restatement; FMA and fp32 identical bits
+    to the default configuration (the same per-output operation sequence, only LDS addresses move)."""
+    import torch
+    with engine.options(VW_FORCE_TILED=1):
+        for w, n, J in [(Daubechies.DB8, 1 << 15, 9), (Daubechies.DB4, 12288, 8), (Symlet.SYM8, 1 << 14, 6)]:
+            x = signals(2, n, 37)
+            tx = vw.MultiLevelMODWTTransform(w, vw.BoundaryMode.PERIODIC)
+            res = tx.decompose(x, J)
+            with engine.options(**opts):
+                y = tx.reconstruct(res)
+            for b in range(2):
+                d, a = O.decompose(x[b], *lohi(w), O.PERIODIC, J)
+                exact(y[b], O.reconstruct(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC))
+        for w, n, J, dt in [(Daubechies.DB8, 1 << 15, 10, torch.float64), (Coiflet.COIF5, 1 << 15, 7, torch.float32)]:
+            x = torch.empty((3, n), dtype=dt, device="cuda")
+            engine.fill_uniform(x, 8)
+            rl, rh = w.lowPassReconstruction(), w.highPassReconstruction()
+            d1, a1 = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, J, nat.FLAG_FMA)
+            y0 = engine.inverse(d1, a1, rl, rh, w.wavelet_id, O.PERIODIC, J, nat.FLAG_FMA)
+            with engine.options(**opts):
+                y1 = engine.inverse(d1, a1, rl, rh, w.wavelet_id, O.PERIODIC, J, nat.FLAG_FMA)
+            torch.cuda.synchronize()
+            assert torch.equal(y0, y1), (w.name(), dt)
+
+
 # ---- alternative fused inverse kernels (selected by policy or option) ------------------------------------
 @pytest.mark.parametrize("opts", [dict(VW_INV_BUF=1), dict(VW_INV_BUF=2), dict(VW_NV=8), dict(VW_INV_BUF=1, VW_NV=8),
                                   dict(VW_INV_NV=2), dict(VW_INV_NV=2, VW_INV_BUF=1), dict(VW_INV_NV=2, VW_INV_BUF=2)],

@@ -78,6 +78,8 @@ struct Tuning {
   int inv_tile = 0;        // VW_INV_TILE: per-level inverse tile (0 = 1024)
   int multi_rblk = 1;      // VW_MULTI_RBLK: register-blocked taps in k_inverse_multi
   int multi_pf = 1;        // VW_MULTI_PF: k_inverse_multi prefetches the next detail tile
+  int multi_pad = 1;       // VW_MULTI_PAD: k_inverse_multi's padded LDS layout at register-blocked levels
+  int multi_inv_tile = 0;  // VW_MULTI_INV_TILE: k_inverse_multi's tile (0 = VW_MULTI_TILE's)
   bool no_sweep = false;   // VW_NO_SWEEP: no column sweeps for deep levels
   int sweep_qc = kSweepChunk;  // VW_SWEEP_QC: q-chunk per sweep thread
   int unroll_max = kMaxTaps;   // VW_UNROLL_MAX: longest filter that runs the tap-unrolled fused kernels
@@ -113,6 +115,8 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_INV_TILE") t.inv_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI_RBLK") t.multi_rblk = v < 0 ? d.multi_rblk : v;
   else if (k == "VW_MULTI_PF") t.multi_pf = v < 0 ? d.multi_pf : v;
+  else if (k == "VW_MULTI_PAD") t.multi_pad = v < 0 ? d.multi_pad : v;
+  else if (k == "VW_MULTI_INV_TILE") t.multi_inv_tile = v < 0 ? 0 : v;
   else if (k == "VW_NO_SWEEP") t.no_sweep = v > 0;
   else if (k == "VW_SWEEP_QC") t.sweep_qc = v >= 16 ? v : d.sweep_qc;
   else if (k == "VW_UNROLL_MAX") t.unroll_max = v < 0 ? d.unroll_max : v;
@@ -131,7 +135,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
 
 static const char* const kTuningKeys[] = {
     "VW_NV", "VW_FWD_PERSIST", "VW_FWD_BUF", "VW_FORCE_TILED", "VW_FWD_REV", "VW_INV_REV",
-    "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_MULTI_PF", "VW_NO_SWEEP", "VW_SWEEP_QC",
+    "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_MULTI_PF", "VW_MULTI_PAD", "VW_MULTI_INV_TILE", "VW_NO_SWEEP", "VW_SWEEP_QC",
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV"};
 
@@ -1260,7 +1264,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     T* tmp[2] = {reinterpret_cast<T*>(c->ws), reinterpret_cast<T*>(c->ws) + plane};
     const T* cur = approx_zero ? nullptr : approx;
     // multi-level groups (PERIODIC sequential sums): start level of the group whose top is j
-    const int mtile = multi_tile<T>(tu);
+    const int mtile = tu.multi_inv_tile >= 64 * V ? tu.multi_inv_tile / V * V : multi_tile<T>(tu);
     const std::vector<int> groups = level_groups(tu, lv, J, L, V, mtile, !pair && boundary == VW_PERIODIC);
     std::vector<int> start_of(J + 1, 0);
     for (int j = 1; j <= J; ++j) {
@@ -1322,6 +1326,13 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         m.rblk = tu.multi_rblk;
         // register prefetch of d_{j-1} while level j computes: whole vectors, every tile of the group
         m.pf = tu.multi_pf && m.vec_io && (int64_t)(mtile + m.ext[g - 1]) / V <= (int64_t)kMultiPF * 256;
+        // padded layout at the register-blocked levels (vw_device.h k_inverse_multi): needs the register
+        // paths (prefetch, blocked taps); the regions grow by one vector in eight
+        m.pad = tu.multi_pad && m.pf && m.rblk && has_unrolled_taps(L);
+        if (m.pad) {
+          const int nvmax = (mtile + m.ext[g - 1]) / V + 1;
+          m.region = (nvmax + nvmax / 8 + 1) * V;
+        }
         copy_taps(m.lo, lo, L);
         copy_taps(m.hi, hi, L);
         LaunchTimer lt(c, "inverse_level");

@@ -1788,6 +1788,16 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
   // The loads are unconditional (clamped vector index): an exec-masked load block makes the waitcnt
   // pass wait for it at the first LDS read.
   const bool pf = p.pf != 0;
+  // Padded LDS layout (p.pad, host contract: pf and rblk on): the register-blocked levels (vector
+  // stride m = s/V in 1..8) read lanes NI*m vectors apart -- an 8-way bank conflict at m = 1 in the
+  // natural layout (62 % of LDS cycles in conflicts on db8 levels 1-5, profiles/r03/pmc_db8_stream.txt).
+  // Level k's A and D then hold logical vector u at u + u/8 (blk_layout's NV = 8 layout: conflict-free
+  // ds_read_b128 at every m <= 8); levels with m = 0 or m >= 16 keep the natural layout.
+  auto padded = [&](int k) {
+    const int sk = p.s0 << k;
+    return p.pad != 0 && sk >= V && sk % V == 0 && sk / V < 16;
+  };
+  auto phys = [&](int u, bool pd) { return pd ? u + (u >> 3) : u; };
   vec dreg[kMultiPF];
   auto d_load = [&](int k) {
     const T* sd = p.src_d[k];
@@ -1805,6 +1815,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
     }
   };
   auto d_store = [&](int k) {
+    const bool pd = padded(k);
     const T* th = p.thr[k];
     const T thb = th ? th[b] : T(0);
     const int nvd = (span + p.ext[k]) / V;
@@ -1816,12 +1827,34 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
         if (th)
 #pragma unroll
           for (int e = 0; e < V; ++e) v[e] = threshold_t(v[e], thb, p.soft);
-        *reinterpret_cast<vec*>(D + w * V) = v;
+        *reinterpret_cast<vec*>(D + phys(w, pd) * V) = v;
       }
     }
   };
-  tile_to_lds(A, p.src_a ? p.src_a + b * (size_t)N : p.src_a, N, ts, 0, span + p.ext[top], kHaloPeriodic, 0,
-              (const T*)nullptr, 0, (const T*)nullptr, T(0), 0, p.src_a == nullptr, vec_ok);
+  if (p.pad) {
+    // a_top through registers into level top's layout (the d_load path, no threshold)
+    const bool pd = padded(top);
+    const int nva = (span + p.ext[top]) / V;
+#pragma unroll
+    for (int i = 0; i < kMultiPF; ++i) {
+      const int w = min((int)threadIdx.x + i * 256, nva - 1);
+      int pos = ts + w * V;
+      if (pos >= N) pos %= N;
+      if (p.src_a)
+        dreg[i] = __builtin_nontemporal_load(reinterpret_cast<const vec*>(p.src_a + b * (size_t)N + pos));
+      else
+#pragma unroll
+        for (int e = 0; e < V; ++e) dreg[i][e] = T(0);
+    }
+#pragma unroll
+    for (int i = 0; i < kMultiPF; ++i) {
+      const int w = (int)threadIdx.x + i * 256;
+      if (w < nva) *reinterpret_cast<vec*>(A + phys(w, pd) * V) = dreg[i];
+    }
+  } else {
+    tile_to_lds(A, p.src_a ? p.src_a + b * (size_t)N : p.src_a, N, ts, 0, span + p.ext[top], kHaloPeriodic, 0,
+                (const T*)nullptr, 0, (const T*)nullptr, T(0), 0, p.src_a == nullptr, vec_ok);
+  }
   if (pf) {
     d_load(top);
     d_store(top);
@@ -1848,6 +1881,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
         const int pr = threadIdx.x;
         const int vb = (pr / m) * m * NI + pr % m;
         const int lim = (span + p.ext[k]) / V - 1;  // last vector of the A/D regions
+        const bool pdk = padded(k), pdn = k > 0 && padded(k - 1);
 #pragma unroll
         for (int r = 0; r < NI; ++r)
 #pragma unroll
@@ -1859,7 +1893,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
             const T* f = br == 0 ? p.lo : p.hi;
 #pragma unroll
             for (int j = 0; j < NI + L - 1; ++j) {
-              const vec x = *reinterpret_cast<const vec*>(buf + min(vb + m * j, lim) * V);
+              const vec x = *reinterpret_cast<const vec*>(buf + phys(min(vb + m * j, lim), pdk) * V);
 #pragma unroll
               for (int r = 0; r < NI; ++r) {
                 const int i = j - r;
@@ -1884,7 +1918,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
               vec o;
 #pragma unroll
               for (int e = 0; e < V; ++e) o[e] = acc[r][e];
-              *reinterpret_cast<vec*>(A + (vb + m * r) * V) = o;
+              *reinterpret_cast<vec*>(A + phys(vb + m * r, pdn) * V) = o;
             }
           }
         }
@@ -1907,6 +1941,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
     }
     if (k == 0) break;
     lds_barrier();  // every read of A and D done
+    const bool pdn = padded(k - 1);  // (this level itself is never padded: see padded())
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int w = threadIdx.x + i * 256;
@@ -1914,7 +1949,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
         vec o;
 #pragma unroll
         for (int e = 0; e < V; ++e) o[e] = acc[i][e];
-        *reinterpret_cast<vec*>(A + w * V) = o;
+        *reinterpret_cast<vec*>(A + phys(w, pdn) * V) = o;
       }
     }
     if (pf) d_store(k - 1);

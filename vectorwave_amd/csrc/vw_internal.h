@@ -151,6 +151,7 @@ struct MultiArgs {
   int taps;
   int rblk;                  // inverse: register-blocked taps where S is a multiple of V
   int pf;                    // inverse: next level's detail tile prefetched into registers
+  int pad;                   // inverse: padded LDS layout at the register-blocked levels (needs pf, rblk)
   T lo[kMaxTaps];
   T hi[kMaxTaps];
 };
