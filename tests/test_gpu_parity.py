@@ -677,15 +677,17 @@ def test_blocked_kernels_match_default(engine, case, fma):
     x = torch.from_numpy(O.fill_uniform(B * n, 9).reshape(B, n)).to(dtype).cuda()
     flags = nat.FLAG_FMA if fma else 0
     out = {}
-    for blk in (0, 2):
-        with engine.options(VW_BLK=blk):
+    # 8: the blocked forward at NV = 8 too (1024-thread workgroups; VW_BLK_FWD8)
+    for blk in (0, 2, 8):
+        with engine.options(VW_BLK=min(blk, 2), VW_BLK_FWD8=int(blk == 8)):
             d, a = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, J, flags)
             y = engine.inverse(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), w.wavelet_id, O.PERIODIC,
                                J, flags)
             torch.cuda.synchronize()
             out[blk] = (d, a, y)
-    for t0, t1 in zip(out[0], out[2]):
-        assert torch.equal(t0, t1)
+    for v in (2, 8):
+        for t0, t1 in zip(out[0], out[v]):
+            assert torch.equal(t0, t1), v
     if dt == "f64" and not fma:
         d, a, y = (t.cpu().numpy() for t in out[2])
         xh = x.cpu().numpy()

@@ -94,6 +94,10 @@ struct Tuning {
   int deep_pf_inv = 1;
   int fwd_nv = 0;              // VW_FWD_NV / VW_INV_NV = 2: 1024-thread fused kernels with 2 vectors per
   int inv_nv = 0;              // thread (L <= 8, unrolled); 0 = policy
+  int sweep2 = 1;              // VW_SWEEP2=0: one column sweep per deep inverse level (no level pairs)
+  int sweep2_ka = 8;           // VW_SWEEP2_KA: stage-A outputs per thread and step (8 or 16)
+  int sweep2_uc = 512;         // VW_SWEEP2_UC: u positions per workgroup chunk
+  int blk_fwd8 = 0;            // VW_BLK_FWD8=1: register-blocked forward at NV = 8 (1024-thread workgroups)
 };
 
 // One switch of the Tuning struct by its environment name; value < 0 = the default.  Returns false
@@ -129,6 +133,10 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_DEEP_PF_INV") t.deep_pf_inv = v <= 0 ? d.deep_pf_inv : std::min(v, 16);
   else if (k == "VW_FWD_NV") t.fwd_nv = v < 0 ? d.fwd_nv : v;
   else if (k == "VW_INV_NV") t.inv_nv = v < 0 ? d.inv_nv : v;
+  else if (k == "VW_SWEEP2") t.sweep2 = v < 0 ? d.sweep2 : v;
+  else if (k == "VW_SWEEP2_KA") t.sweep2_ka = v == 16 ? 16 : v == 8 ? 8 : d.sweep2_ka;
+  else if (k == "VW_SWEEP2_UC") t.sweep2_uc = v >= 32 ? v : d.sweep2_uc;
+  else if (k == "VW_BLK_FWD8") t.blk_fwd8 = v < 0 ? d.blk_fwd8 : v;
   else return false;
   return true;
 }
@@ -137,7 +145,8 @@ static const char* const kTuningKeys[] = {
     "VW_NV", "VW_FWD_PERSIST", "VW_FWD_BUF", "VW_FORCE_TILED", "VW_FWD_REV", "VW_INV_REV",
     "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_MULTI_PF", "VW_MULTI_PAD", "VW_MULTI_INV_TILE", "VW_NO_SWEEP", "VW_SWEEP_QC",
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
-    "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV"};
+    "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
+    "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_BLK_FWD8"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -970,9 +979,11 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     const bool persist = dbl && a.unrolled && persist_ok(threads, nv, fit);
     // register-blocked PERIODIC forward for long filters (vw_device.h k_forward_blk): padded layouts
     int blk_lds = 0;
-    // (NV = 8: 1024-thread workgroups cap a lane at 128 VGPRs and the blocked forward spills there --
-    // measured 2x slower at sym8 N = 16384; the one-vector-per-tap kernel runs instead)
-    if (tu.blk > 0 && L >= tu.blk && a.unrolled && !validate && !hist && (int64_t)threads * nv == nvec && nv == 4) {
+    // (NV = 8: 1024-thread workgroups cap a lane at 128 VGPRs; without spills since round 3, but still
+    // measured slower at sym8 N = 16384 (forward 5.38-5.42 vs 5.15-5.24 ms, profiles/r03/ab_blk_fwd8_sym8.log):
+    // the one-vector-per-tap kernel runs unless VW_BLK_FWD8=1)
+    if (tu.blk > 0 && L >= tu.blk && a.unrolled && !validate && !hist && (int64_t)threads * nv == nvec &&
+        (nv == 4 || (nv == 8 && tu.blk_fwd8))) {
       bool okb = true;
       int hlv = 0;
       for (int j = 0; j < J; ++j) {
@@ -1341,6 +1352,42 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         cur = m.out_a;
         j = j0;
         continue;
+      }
+      // two column-sweep levels per launch (k_inverse_sweep2): a_{j-1} stays in LDS
+      if (tu.sweep2 && !tu.deep_inv && !tu.no_sweep && !pair && j >= 2 && has_unrolled_taps(L) && !in_group[j - 1] &&
+          start_of[j - 1] == 0) {
+        const LevelDesc& lj = lv[j - 1];
+        const LevelDesc& lh = lv[j - 2];
+        const int ka = L <= 17 ? tu.sweep2_ka : 16, kb = 2 * ka;
+        const int64_t s = lj.s, h = lh.s;
+        auto plain = [](const LevelDesc& d) {
+          return d.mode == kHaloPeriodic && d.dir_a == 1 && d.dir_d == 1 && d.off_a == 0 && d.off_d == 0;
+        };
+        if (s == 2 * h && h >= kSweepMinS && h % 64 == 0 && N % s == 0 && (int64_t)(kb + L) * s <= N &&
+            kb >= L - 1 && plain(lj) && plain(lh)) {
+          LevelArgs<T> a;
+          memset(&a, 0, sizeof(a));
+          a.lv = lj;
+          a.src_a = cur;
+          a.src_d = lj.use_d ? details + (size_t)(j - 1) * plane : nullptr;
+          a.use_d = lj.use_d;
+          a.src_d2 = lh.use_d ? details + (size_t)(j - 2) * plane : nullptr;
+          a.use_d2 = lh.use_d;
+          a.thr = thr ? thr + (size_t)(j - 1) * (size_t)thr_ld : nullptr;
+          a.thr2 = thr ? thr + (size_t)(j - 2) * (size_t)thr_ld : nullptr;
+          a.soft = soft;
+          a.out_a = (j == 2) ? y : nxt;
+          a.B = B; a.N = (int)N; a.taps = L;
+          a.tile = (int)round_up(tu.sweep2_uc, kb);
+          copy_taps(a.lo, lo, L);
+          copy_taps(a.hi, hi, L);
+          LaunchTimer lt(c, "inverse_level");
+          hipError_t e = launch_inverse_sweep2<T>(a, ka, fma, c->stream);
+          if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse level-pair launch failed: %s", hipGetErrorString(e));
+          cur = a.out_a;
+          --j;  // level j-1 done too
+          continue;
+        }
       }
       LevelArgs<T> a;
       memset(&a, 0, sizeof(a));

@@ -1148,6 +1148,48 @@ __device__ __forceinline__ void blk_inv_branch_c(const T* Rb, const T* f, T (&ac
     for (int e = 0; e < V; ++e) asm volatile("" : "+v"(acc[r][e]));
 }
 
+// blk_inv_branch with wave-uniform offsets: under the same condition as BlkC::ok (the pad groups
+// align with a thread's block), the physical offset of logical vector vb + q*m from vb's is
+// q*m + ((q*m) >> sh)*pad for every thread -- a scalar value per read, so a read costs one vector
+// add (base + scalar offset) instead of the per-lane shift / multiply / add of blk_phys.  One code
+// copy for every stride (the compile-time forms, one copy per m, measured slower at NV = 8).
+template <typename T, int L, bool FMA, int NV>
+__device__ __forceinline__ void blk_inv_branch_s(const T* Rb, int m, int sh, int pad, const T* f,
+                                                 T (&acc)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  constexpr int TC = blk_chunk<T, NV>();
+  static_for<0, (L + TC - 1) / TC>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * TC;
+    constexpr int I1 = (I0 + TC < L) ? I0 + TC : L;
+    T fc[I1 - I0];
+#pragma unroll
+    for (int i = I0; i < I1; ++i) fc[i - I0] = f[i];
+#pragma unroll
+    for (int q = I0; q < I1 + NV - 1; ++q) {
+      const int qm = __builtin_amdgcn_readfirstlane(q * m);
+      const int off = __builtin_amdgcn_readfirstlane(qm + (qm >> sh) * pad);
+      const vec x = *reinterpret_cast<const vec*>(Rb + off * V);
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        const int i = q - r;
+        if (i >= I0 && i < I1) {
+          vmadd<FMA>(acc[r], x, fc[i - I0]);
+        }
+      }
+      if (((q - I0) & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+#pragma unroll
+  for (int r = 0; r < NV; ++r)
+#pragma unroll
+    for (int e = 0; e < V; ++e) asm volatile("" : "+v"(acc[r][e]));
+}
+
+#ifndef VW_BLK_SOFF
+#define VW_BLK_SOFF 1  // NV = 8 inverse branch: wave-uniform offsets where the layout allows (0: per-lane blk_phys)
+#endif
+
 // One inverse branch at vector stride m >= 1: the compile-time forms for m = 1..64 (immediate LDS
 // offsets stay below 64 KiB for L <= 30), the generic one otherwise.  Same reads, same sums.
 template <typename T, int L, bool FMA, int NV>
@@ -1155,8 +1197,13 @@ __device__ __forceinline__ void blk_inv_any(const T* R, const BlkLayout& lo, int
                                             T (&acc)[NV][VT<T>::V]) {
   constexpr int V = VT<T>::V;
   if constexpr (NV >= 8) {
-    // measured slower at NV = 8 (sym8 fp64 inverse 7.18 -> 8.08 ms, profiles/r03/ab_sym8_cinv.log)
-    blk_inv_branch<T, L, FMA, NV>(R, lo, vb, m, f, acc);
+    // compile-time forms measured slower at NV = 8 (sym8 fp64 inverse 7.18 -> 8.08 ms,
+    // profiles/r03/ab_sym8_cinv.log)
+    const int sh = __builtin_amdgcn_readfirstlane(lo.sh), pad = __builtin_amdgcn_readfirstlane(lo.pad);
+    if (VW_BLK_SOFF && (pad == 0 || ((m * NV) & ((1 << sh) - 1)) == 0))
+      blk_inv_branch_s<T, L, FMA, NV>(R + blk_phys(lo, vb) * V, m, sh, pad, f, acc);
+    else
+      blk_inv_branch<T, L, FMA, NV>(R, lo, vb, m, f, acc);
   } else {
     const T* Rb = R + blk_phys(lo, vb) * V;
     auto go = [&](auto mc, auto tc) __attribute__((always_inline)) {
@@ -1707,6 +1754,132 @@ __global__ void __launch_bounds__(256) k_inverse_sweep(const LevelArgs<T> p) {
     }
     A.shift();
     D.shift();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Two inverse levels per launch: level j (spacing s = 2h) and level j-1 (spacing h), PERIODIC,
+// sequential sums (K4: MultiLevelMODWTTransform.java:576-589), as two column sweeps chained through
+// an LDS ring, so a_{j-1} never goes to HBM (4 rows per pair of levels instead of 6).
+//
+// In the residue class r mod h, position u is the sample t = r + u*h (u < nu = N/h); level j-1 reads
+// u + i, level j reads u + 2i -- i.e. level j is a plain sweep over each of the two parity classes
+// (r + e*h mod s, u = 2v + e).  A workgroup owns 64 consecutive residues (one fp64 per lane: 512
+// contiguous bytes per wave access) of one signal and a chunk [u0, u1) of u:
+//   waves 0, 1 (stage A): parity e = wave, a register-window sweep of level j (as k_inverse_sweep),
+//     writing a_{j-1} of block n (KB = 2*KA positions) into the ring at step n;
+//   waves 2, 3 (stage B): at step n, half of block n-2 of level j-1: a_{j-1}[u + i] from the ring
+//     (it reaches into block n-1, which is complete), d_{j-1} from HBM, y = a_{j-2} to HBM.
+// One barrier per step; the ring holds blocks n-2 .. n.  Stage A runs one block past the chunk (the
+// reach of level j-1, L-1 <= KB positions) and wraps mod N: every value equals the reference's (t+l)%N
+// read, products summed in the same order -> bit-exact in EXACT mode.
+// Host contract (vw_capi.cpp): h % 64 == 0, N % s == 0, both levels PERIODIC / dir +1 / offset 0,
+// (KB + L) * s <= N (one wrap at most), p.tile (u per chunk) a multiple of KB.
+constexpr int kSweep2Threads = 256;
+
+template <typename T, int L, bool FMA, int KA>
+__global__ void __launch_bounds__(kSweep2Threads) k_inverse_sweep2(const LevelArgs<T> p) {
+  constexpr int KB = 2 * KA;
+  constexpr int RING = 3 * KB;
+  static_assert(KB >= L - 1, "level j-1 reads at most one block ahead");
+  __shared__ T ring[RING * 64];
+  const int s = p.lv.s, h = s >> 1, N = p.N;
+  const int nu = N / h;
+  const int nrb = h >> 6;
+  const int uc = p.tile;
+  const int nch = (nu + uc - 1) / uc;
+  long long id = blockIdx.x;
+  const int ch = (int)(id % nch);
+  id /= nch;
+  const int rb = (int)(id % nrb);
+  const long long b = id / nrb;
+  if (b >= p.B) return;  // workgroup-uniform
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int r = rb * 64 + lane;
+  const int u0 = ch * uc, u1 = min(u0 + uc, nu);
+  const int nblk = (u1 - u0 + KB - 1) / KB;
+  const size_t row = (size_t)b * (size_t)N;
+  auto wrap = [&](long long t) -> long long { return t >= N ? t - N : t; };
+  if (wave < 2) {
+    // ---- stage A: level j over parity class e (t = r + e*h + v*s), blocks 0 .. nblk
+    const int e = wave;
+    const T thr_b = p.thr ? p.thr[b] : T(0);
+    const T* sa = p.src_a ? p.src_a + row : nullptr;
+    const T* sd = (p.src_d && p.use_d) ? p.src_d + row : nullptr;
+    auto fa = [&](long long t) -> T { return sa ? sa[wrap(t)] : T(0); };
+    auto fd = [&](long long t) -> T {
+      if (!sd) return T(0);
+      const T v = sd[wrap(t)];
+      return p.thr ? threshold_t(v, thr_b, p.soft) : v;
+    };
+    SweepWin<T, L, KA, 1> A, D;
+    long long tb = (long long)r + (long long)e * h + (long long)(u0 >> 1) * s;
+    A.fill_head(tb, s, 0, fa);
+    D.fill_head(tb, s, 0, fd);
+    for (int n = 0; n <= nblk + 1; ++n) {
+      if (n <= nblk) {
+        A.load_block(tb, s, 0, fa);
+        D.load_block(tb, s, 0, fd);
+        T* rn = ring + (n % 3) * KB * 64 + e * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < KA; ++k) {
+          T acc = T(0);
+#pragma unroll
+          for (int i = 0; i < L; ++i) acc = madd<FMA>(acc, A.tap(k, i), p.lo[i]);
+#pragma unroll
+          for (int i = 0; i < L; ++i) acc = madd<FMA>(acc, D.tap(k, i), p.hi[i]);
+          rn[2 * k * 64] = acc;  // u = u0 + n*KB + 2k + e
+        }
+        A.shift();
+        D.shift();
+        tb += (long long)KA * s;
+      }
+      __syncthreads();
+    }
+  } else {
+    // ---- stage B: level j-1 over class r mod h, half hh of block n-2 at step n
+    const int hh = wave - 2;
+    const T thr_b = p.thr2 ? p.thr2[b] : T(0);
+    const T* sd = (p.src_d2 && p.use_d2) ? p.src_d2 + row : nullptr;
+    T* y = p.out_a + row;
+    for (int n = 0; n <= nblk + 1; ++n) {
+      if (n >= 2) {
+        const int m = n - 2;
+        const int ub = u0 + m * KB + hh * KA;  // first output u of this half-block
+        const int sb = (m % 3) * KB + hh * KA;  // its ring slot
+        T w[KA + L - 1];
+        T acc[KA];
+        // d_{j-1} window first: its loads are in flight during the approximation branch
+        T wd[KA + L - 1];
+#pragma unroll
+        for (int x = 0; x < KA + L - 1; ++x) {
+          if (sd) {
+            const T v = sd[wrap((long long)r + (long long)(ub + x) * h)];
+            wd[x] = p.thr2 ? threshold_t(v, thr_b, p.soft) : v;
+          } else {
+            wd[x] = T(0);
+          }
+        }
+#pragma unroll
+        for (int x = 0; x < KA + L - 1; ++x) {
+          const int sl = sb + x;
+          w[x] = ring[(sl >= RING ? sl - RING : sl) * 64 + lane];
+        }
+#pragma unroll
+        for (int k = 0; k < KA; ++k) {
+          acc[k] = T(0);
+#pragma unroll
+          for (int i = 0; i < L; ++i) acc[k] = madd<FMA>(acc[k], w[k + i], p.lo[i]);
+        }
+#pragma unroll
+        for (int k = 0; k < KA; ++k) {
+#pragma unroll
+          for (int i = 0; i < L; ++i) acc[k] = madd<FMA>(acc[k], wd[k + i], p.hi[i]);
+          if (ub + k < u1) y[(size_t)r + (size_t)(ub + k) * (size_t)h] = acc[k];
+        }
+      }
+      __syncthreads();
+    }
   }
 }
 

@@ -81,6 +81,32 @@ hipError_t launch_inverse_sweep(const LevelArgs<T>& a, bool fma, hipStream_t st)
 template hipError_t launch_forward_sweep<VW_T>(const LevelArgs<VW_T>&, bool, hipStream_t);
 template hipError_t launch_inverse_sweep<VW_T>(const LevelArgs<VW_T>&, bool, hipStream_t);
 
+// Two inverse levels per launch (k_inverse_sweep2): one workgroup per (signal, 64-residue block,
+// u-chunk).  KA = 8 or 16 outputs per stage-A thread and step.
+template <typename T, int L, bool FMA, int KA>
+static hipError_t run_inverse_sweep2(const LevelArgs<T>& a, hipStream_t st) {
+  const long long h = a.lv.s / 2, nu = a.N / h, nch = (nu + a.tile - 1) / a.tile;
+  const long long groups = a.B * (h / 64) * nch;
+  hipLaunchKernelGGL((k_inverse_sweep2<T, L, FMA, KA>), dim3((unsigned)groups), dim3(kSweep2Threads), 0, st, a);
+  return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_inverse_sweep2(const LevelArgs<T>& a, int ka, bool fma, hipStream_t st) {
+  switch (a.taps) {
+#define VW_CASE(n)                                                                                  \
+    case n:                                                                                         \
+      if constexpr (n <= 17) {                                                                      \
+        if (ka == 8) return fma ? run_inverse_sweep2<T, n, true, 8>(a, st) : run_inverse_sweep2<T, n, false, 8>(a, st); \
+      }                                                                                             \
+      return fma ? run_inverse_sweep2<T, n, true, 16>(a, st) : run_inverse_sweep2<T, n, false, 16>(a, st);
+    VW_TAP_LIST(VW_CASE)
+#undef VW_CASE
+    default: return hipErrorInvalidValue;
+  }
+}
+template hipError_t launch_inverse_sweep2<VW_T>(const LevelArgs<VW_T>&, int, bool, hipStream_t);
+
 template <typename T>
 hipError_t launch_forward_level(const LevelArgs<T>& a, int lds, bool fma, hipStream_t st) {
   return dispatch_level<T, false>(a, lds, fma, st);
