@@ -1,10 +1,11 @@
-"""Level-pair inverse sweeps (vw_device.h k_inverse_sweep2): two deep PERIODIC inverse levels j, j-1 in
-one launch, a_{j-1} handed from the level-j column sweep to the level-(j-1) sweep through an LDS ring.
+"""Chained inverse column sweeps (vw_device.h k_inverse_sweep2 / k_inverse_sweep3): two or three deep
+PERIODIC inverse levels in one launch, the intermediate approximations handed from one level's column
+sweep to the next through LDS rings (VW_SWEEP2 = 2: pairs only, 3: triples where they qualify).
 EXACT: bit-exact against the restatement of vectorwave-core (MultiLevelMODWTTransform.java:339-349,
 :576-589); FMA and fp32: identical bits to one column sweep per level (VW_SWEEP2=0), since every output
-is the same operation sequence.  Shapes cover several pairs, a pair above a lone sweep level, N not a
-power of two (partial u-chunks), short and long filters (KA = 8 / 16), small chunks, masked details,
-a zero approximation and the fused denoise thresholds."""
+is the same operation sequence.  Shapes cover triples, pairs of 64- and 32-residue groups, a lone sweep
+level, N not a power of two (partial u-chunks), short and long filters (KA = 8 / 16), small chunks,
+masked details, a zero approximation and the fused denoise thresholds."""
 import numpy as np
 import pytest
 
@@ -35,15 +36,17 @@ def lohi_r(w):
 def test_pair_inverse_bit_exact(engine, w, n, J, B):
     x = _rows(B, n, 7)
     d, a = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, J, 0)        # BatchMODWT semantics (no cap)
-    with engine.options(VW_SWEEP2=1):
-        y = engine.inverse(d, a, *lohi_r(w), w.wavelet_id, O.PERIODIC, J, 0)
-    for b in range(B):
-        y_ref = O.reconstruct(d[:, b, :], a[b], *lohi_r(w), O.PERIODIC)
-        assert np.array_equal(y[b], y_ref), b
+    for g in (3, 2):
+        with engine.options(VW_SWEEP2=g):
+            y = engine.inverse(d, a, *lohi_r(w), w.wavelet_id, O.PERIODIC, J, 0)
+        for b in range(B):
+            y_ref = O.reconstruct(d[:, b, :], a[b], *lohi_r(w), O.PERIODIC)
+            assert np.array_equal(y[b], y_ref), (g, b)
 
 
-@pytest.mark.parametrize("opts", [{}, {"VW_SWEEP2_KA": 16}, {"VW_SWEEP2_UC": 32}, {"VW_SWEEP2_UC": 4096}],
-                         ids=["default", "ka16", "uc32", "uc4096"])
+@pytest.mark.parametrize("opts", [{"VW_SWEEP2": 3}, {"VW_SWEEP2": 2}, {"VW_SWEEP2": 3, "VW_SWEEP2_KA": 16},
+                                  {"VW_SWEEP2": 3, "VW_SWEEP2_UC": 32}, {"VW_SWEEP2": 2, "VW_SWEEP2_UC": 4096}],
+                         ids=["triple", "pair", "ka16", "uc32", "pair-uc4096"])
 @pytest.mark.parametrize("w,n,J,dt", [(Daubechies.DB8, 1 << 16, 10, "f64"), (Coiflet.COIF5, 1 << 16, 9, "f32"),
                                       (Daubechies.DB4, 3 << 15, 11, "f32"), (Haar.INSTANCE, 1 << 15, 13, "f64")])
 def test_pair_matches_single_sweeps(engine, opts, w, n, J, dt):
@@ -53,7 +56,7 @@ def test_pair_matches_single_sweeps(engine, opts, w, n, J, dt):
     engine.fill_uniform(x, 11)
     for flags in (0, nat.FLAG_FMA):
         d, a = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, J, flags)
-        with engine.options(VW_SWEEP2=1, **opts):
+        with engine.options(**opts):
             y1 = engine.inverse(d, a, *lohi_r(w), w.wavelet_id, O.PERIODIC, J, flags)
         with engine.options(VW_SWEEP2=0):
             y0 = engine.inverse(d, a, *lohi_r(w), w.wavelet_id, O.PERIODIC, J, flags)
@@ -68,7 +71,7 @@ def test_pair_partial_reconstruction(engine):
     n, J = 1 << 15, 10
     x = _rows(2, n, 17)
     d, a = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, J, 0)
-    with engine.options(VW_SWEEP2=1):
+    with engine.options(VW_SWEEP2=3):
         for mask, az in [(0b1000000000, False), (0b0110000000, True), (0b0101010101, False), (0, False)]:
             y = engine.inverse(d, a, *lohi_r(w), w.wavelet_id, O.PERIODIC, J, 0, detail_mask=mask, approx_zero=az)
             for b in range(2):
@@ -82,7 +85,7 @@ def test_pair_denoise_thresholds(engine):
     w = Symlet.SYM8
     n, J = 1 << 16, 9
     x = _rows(2, n, 31)
-    with engine.options(VW_SWEEP2=1):
+    with engine.options(VW_SWEEP2=3):
         y, thr = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC).denoise(x, J, return_thresholds=True)
     for b in range(2):
         y_ref, t_ref = O.swt_denoise(x[b], *lohi(w), O.PERIODIC, J, wavelet_id=w.wavelet_id)

@@ -94,9 +94,11 @@ struct Tuning {
   int deep_pf_inv = 1;
   int fwd_nv = 0;              // VW_FWD_NV / VW_INV_NV = 2: 1024-thread fused kernels with 2 vectors per
   int inv_nv = 0;              // thread (L <= 8, unrolled); 0 = policy
-  int sweep2 = 1;              // VW_SWEEP2=0: one column sweep per deep inverse level (no level pairs)
+  int sweep2 = 3;              // VW_SWEEP2: deep inverse column-sweep levels chained per launch, up to 3 (2 = pairs only,
+                               // 0 = one sweep per level)
   int sweep2_ka = 8;           // VW_SWEEP2_KA: stage-A outputs per thread and step (8 or 16)
-  int sweep2_uc = 512;         // VW_SWEEP2_UC: u positions per workgroup chunk
+  int sweep2_uc = 2048;        // VW_SWEEP2_UC: u positions per workgroup chunk (512 / 1024 / 2048: 9.68 / 9.50 / 9.33 ms db8 inverse)
+  int sweep2_r = 0;            // VW_SWEEP2_R=32: 32-residue groups even where h allows 64 (0 = widest)
   int blk_fwd8 = 0;            // VW_BLK_FWD8=1: register-blocked forward at NV = 8 (1024-thread workgroups)
 };
 
@@ -136,6 +138,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_SWEEP2") t.sweep2 = v < 0 ? d.sweep2 : v;
   else if (k == "VW_SWEEP2_KA") t.sweep2_ka = v == 16 ? 16 : v == 8 ? 8 : d.sweep2_ka;
   else if (k == "VW_SWEEP2_UC") t.sweep2_uc = v >= 32 ? v : d.sweep2_uc;
+  else if (k == "VW_SWEEP2_R") t.sweep2_r = v == 32 ? 32 : 0;
   else if (k == "VW_BLK_FWD8") t.blk_fwd8 = v < 0 ? d.blk_fwd8 : v;
   else return false;
   return true;
@@ -146,7 +149,7 @@ static const char* const kTuningKeys[] = {
     "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_MULTI_PF", "VW_MULTI_PAD", "VW_MULTI_INV_TILE", "VW_NO_SWEEP", "VW_SWEEP_QC",
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
-    "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_BLK_FWD8"};
+    "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_BLK_FWD8"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -837,6 +840,40 @@ static std::vector<int> level_groups(const Tuning& tu, const std::vector<LevelDe
   return g;
 }
 
+// Level group of the chained column sweeps (vw_device.h k_inverse_sweep2 / k_inverse_sweep3): inverse levels
+// j .. j-levels+1 (spacings G*h .. h, G = 2 / 4), all column-sweep levels outside the multi-level tile
+// groups, PERIODIC / dir +1 / offset 0.  Picks KA (outputs per thread and step) and R (residues per
+// group, 64 or 32 = h's alignment) under the kernels' rules: a block of G*KA positions covers the
+// reach of the levels below the top (L-1 per level, in the bottom level's positions: 1 / 2 steps), the
+// LDS rings (1 / 2 of 3 blocks x R) fit, and one wrap mod N at most.
+template <typename T>
+static bool sweepg_plan(const Tuning& tu, const std::vector<LevelDesc>& lv, int j, int levels, int L, int64_t N,
+                        const std::vector<char>& in_group, const std::vector<int>& start_of, int* ka_out, int* r_out) {
+  if (levels < 2 || levels > 3 || j < levels) return false;
+  const int G = levels == 2 ? 2 : 4;
+  const int64_t h = lv[j - levels].s;
+  if (h < kSweepMinS || h % 32 != 0 || lv[j - 1].s != G * h) return false;
+  for (int k = j - levels + 1; k <= j; ++k) {
+    const LevelDesc& d = lv[k - 1];
+    if (d.mode != kHaloPeriodic || d.dir_a != 1 || d.dir_d != 1 || d.off_a != 0 || d.off_d != 0) return false;
+    if (k < j && (in_group[k] || start_of[k] != 0)) return false;
+  }
+  const int R = (h % 64 == 0 && tu.sweep2_r != 32) ? 64 : 32;
+  const int kmin = (levels == 2 ? 1 : 2) * (L - 1);
+  for (int ka : {L <= 17 ? tu.sweep2_ka : 16, 16}) {
+    for (int r : {R, 32}) {
+      const int64_t kb = (int64_t)G * ka;
+      const int64_t lds = (levels == 2 ? 1 : 2) * 3 * kb * r * (int64_t)sizeof(T);
+      if (kb < kmin || lds > kLdsBytes || h % r != 0) continue;
+      if (N % (G * h) != 0 || (2 * kb + 2 * L) * G * h > N) continue;
+      *ka_out = ka;
+      *r_out = r;
+      return true;
+    }
+  }
+  return false;
+}
+
 // Streaming deep group (vw_deep.hip): PERIODIC levels jlo..jhi of the per-level path in one launch.
 // Needs level jlo's spacing P to divide N and hold C = 64 bytes of residues; every ring of the group
 // within the LDS budget.  Ring capacities: DMA-fed rings hold their history + two tiles (the next
@@ -1353,39 +1390,41 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         j = j0;
         continue;
       }
-      // two column-sweep levels per launch (k_inverse_sweep2): a_{j-1} stays in LDS
-      if (tu.sweep2 && !tu.deep_inv && !tu.no_sweep && !pair && j >= 2 && has_unrolled_taps(L) && !in_group[j - 1] &&
-          start_of[j - 1] == 0) {
-        const LevelDesc& lj = lv[j - 1];
-        const LevelDesc& lh = lv[j - 2];
-        const int ka = L <= 17 ? tu.sweep2_ka : 16, kb = 2 * ka;
-        const int64_t s = lj.s, h = lh.s;
-        auto plain = [](const LevelDesc& d) {
-          return d.mode == kHaloPeriodic && d.dir_a == 1 && d.dir_d == 1 && d.off_a == 0 && d.off_d == 0;
-        };
-        if (s == 2 * h && h >= kSweepMinS && h % 64 == 0 && N % s == 0 && (int64_t)(kb + L) * s <= N &&
-            kb >= L - 1 && plain(lj) && plain(lh)) {
+      // two or three column-sweep levels per launch (k_inverse_sweep2 / 3): the intermediate
+      // approximations stay in LDS rings
+      if (tu.sweep2 && !tu.deep_inv && !tu.no_sweep && !pair && j >= 2 && has_unrolled_taps(L)) {
+        int G = 0, ka = 0, R = 0;
+        for (int levels = std::min(tu.sweep2 >= 3 ? 3 : 2, j); levels >= 2 && !G; --levels)
+          if (sweepg_plan<T>(tu, lv, j, levels, L, N, in_group, start_of, &ka, &R)) G = levels;
+        if (G) {
+          const LevelDesc& lj = lv[j - 1];
           LevelArgs<T> a;
           memset(&a, 0, sizeof(a));
           a.lv = lj;
           a.src_a = cur;
           a.src_d = lj.use_d ? details + (size_t)(j - 1) * plane : nullptr;
           a.use_d = lj.use_d;
-          a.src_d2 = lh.use_d ? details + (size_t)(j - 2) * plane : nullptr;
-          a.use_d2 = lh.use_d;
           a.thr = thr ? thr + (size_t)(j - 1) * (size_t)thr_ld : nullptr;
+          a.src_d2 = lv[j - 2].use_d ? details + (size_t)(j - 2) * plane : nullptr;
+          a.use_d2 = lv[j - 2].use_d;
           a.thr2 = thr ? thr + (size_t)(j - 2) * (size_t)thr_ld : nullptr;
+          if (G == 3) {
+            a.src_d3 = lv[j - 3].use_d ? details + (size_t)(j - 3) * plane : nullptr;
+            a.use_d3 = lv[j - 3].use_d;
+            a.thr3 = thr ? thr + (size_t)(j - 3) * (size_t)thr_ld : nullptr;
+          }
           a.soft = soft;
-          a.out_a = (j == 2) ? y : nxt;
+          a.out_a = (j == G) ? y : nxt;
           a.B = B; a.N = (int)N; a.taps = L;
+          const int kb = (G == 2 ? 2 : 4) * ka;
           a.tile = (int)round_up(tu.sweep2_uc, kb);
           copy_taps(a.lo, lo, L);
           copy_taps(a.hi, hi, L);
           LaunchTimer lt(c, "inverse_level");
-          hipError_t e = launch_inverse_sweep2<T>(a, ka, fma, c->stream);
-          if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse level-pair launch failed: %s", hipGetErrorString(e));
+          hipError_t e = launch_inverse_sweepg<T>(a, G == 2 ? 2 : 4, ka, R, fma, c->stream);
+          if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse level-group launch failed: %s", hipGetErrorString(e));
           cur = a.out_a;
-          --j;  // level j-1 done too
+          j -= G - 1;  // levels j-1 (, j-2) done too
           continue;
         }
       }

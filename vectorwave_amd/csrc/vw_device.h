@@ -1758,125 +1758,238 @@ __global__ void __launch_bounds__(256) k_inverse_sweep(const LevelArgs<T> p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Two inverse levels per launch: level j (spacing s = 2h) and level j-1 (spacing h), PERIODIC,
-// sequential sums (K4: MultiLevelMODWTTransform.java:576-589), as two column sweeps chained through
-// an LDS ring, so a_{j-1} never goes to HBM (4 rows per pair of levels instead of 6).
+// Two or three inverse levels per launch: levels j, j-1 (, j-2) with spacings G*h .. h (G = 2 or 4),
+// PERIODIC, sequential sums (K4: MultiLevelMODWTTransform.java:576-589), as column sweeps chained
+// through LDS rings, so the intermediate approximations never go to HBM (4 rows per pair of levels
+// instead of 6, 5 per triple instead of 9).
 //
-// In the residue class r mod h, position u is the sample t = r + u*h (u < nu = N/h); level j-1 reads
-// u + i, level j reads u + 2i -- i.e. level j is a plain sweep over each of the two parity classes
-// (r + e*h mod s, u = 2v + e).  A workgroup owns 64 consecutive residues (one fp64 per lane: 512
-// contiguous bytes per wave access) of one signal and a chunk [u0, u1) of u:
-//   waves 0, 1 (stage A): parity e = wave, a register-window sweep of level j (as k_inverse_sweep),
-//     writing a_{j-1} of block n (KB = 2*KA positions) into the ring at step n;
-//   waves 2, 3 (stage B): at step n, half of block n-2 of level j-1: a_{j-1}[u + i] from the ring
-//     (it reaches into block n-1, which is complete), d_{j-1} from HBM, y = a_{j-2} to HBM.
-// One barrier per step; the ring holds blocks n-2 .. n.  Stage A runs one block past the chunk (the
-// reach of level j-1, L-1 <= KB positions) and wraps mod N: every value equals the reference's (t+l)%N
-// read, products summed in the same order -> bit-exact in EXACT mode.
-// Host contract (vw_capi.cpp): h % 64 == 0, N % s == 0, both levels PERIODIC / dir +1 / offset 0,
-// (KB + L) * s <= N (one wrap at most), p.tile (u per chunk) a multiple of KB.
-constexpr int kSweep2Threads = 256;
+// In the residue class r mod h, position u is the sample t = r + u*h (u < nu = N/h); the bottom level
+// reads u + i, the one above u + 2i, the top u + G*i -- so the top level is a plain sweep over each of
+// the G classes u = G*v + e (r + e*h mod G*h).  A workgroup owns R consecutive residues (R = 64: one
+// fp64 per lane, 512 contiguous bytes per wave access; R = 32 where h = 32: two residue groups per
+// wave, 256 B each) of one signal and a chunk [u0, u1) of u, in groups of R threads:
+//   top groups (G of them): group e sweeps class e of the top level with register windows (as
+//     k_inverse_sweep) and writes its KA outputs of block n (KB = G*KA positions) into ring 1 at step n;
+//   middle groups (triple, 4): at step n, level j-1 over block n-2 -- parity e2, half of the parity's
+//     2*KA outputs -- reading a_{j-1}[u + 2i] from ring 1 (it reaches into block n-1, complete) and
+//     d_{j-1} from HBM, writing a_{j-2} into ring 2;
+//   bottom groups (4 of a triple, 2 of a pair): at step 2 (pair) / 4 (triple) behind the top, KA
+//     outputs of the bottom level each, ring -> y in HBM.
+// One barrier per step; every ring holds three blocks.  The upper stages run past the chunk by their
+// reach (L-1 positions at each level below, <= KB) and wrap mod N: every value equals the reference's
+// (t+l)%N read, products summed in the same order -> bit-exact in EXACT mode.
+// Host contract (vw_capi.cpp): h % R == 0, N % (G*h) == 0, every level PERIODIC / dir +1 / offset 0,
+// (2*KB + 2*L) * G*h <= N (one wrap at most), KB >= 2*(L-1), p.tile (u per chunk) a multiple of KB.
 
-template <typename T, int L, bool FMA, int KA>
-__global__ void __launch_bounds__(kSweep2Threads) k_inverse_sweep2(const LevelArgs<T> p) {
-  constexpr int KB = 2 * KA;
-  constexpr int RING = 3 * KB;
-  static_assert(KB >= L - 1, "level j-1 reads at most one block ahead");
-  __shared__ T ring[RING * 64];
-  const int s = p.lv.s, h = s >> 1, N = p.N;
-  const int nu = N / h;
-  const int nrb = h >> 6;
-  const int uc = p.tile;
-  const int nch = (nu + uc - 1) / uc;
+// KA outputs of one level at u = ub + st*k (k < KA, st = the level's spacing in u): a from an LDS ring
+// (slot of ub: sl0, slot stride st), d from HBM at t = tb + x*ts (ts = st*h); the approximation branch,
+// then the detail branch, each i ascending.
+template <typename T, int L, bool FMA, int KA, int R, int RING>
+__device__ __forceinline__ void sweep_ring_stage(const T* ring, int lane, int sl0, int st, const T* sd, bool thr_on,
+                                                 T thr_b, int soft, long long tb, long long ts, int N, const T* lo,
+                                                 const T* hi, T (&acc)[KA]) {
+  T wd[KA + L - 1];
+#pragma unroll
+  for (int x = 0; x < KA + L - 1; ++x) {  // issued first: in flight during the approximation branch
+    if (sd) {
+      long long t = tb + (long long)x * ts;
+      t = t >= N ? t - N : t;
+      const T v = sd[t];
+      wd[x] = thr_on ? threshold_t(v, thr_b, soft) : v;
+    } else {
+      wd[x] = T(0);
+    }
+  }
+  T w[KA + L - 1];
+#pragma unroll
+  for (int x = 0; x < KA + L - 1; ++x) {
+    const int sl = sl0 + x * st;
+    w[x] = ring[(sl >= RING ? sl - RING : sl) * R + lane];
+  }
+#pragma unroll
+  for (int k = 0; k < KA; ++k) {
+    acc[k] = T(0);
+#pragma unroll
+    for (int i = 0; i < L; ++i) acc[k] = madd<FMA>(acc[k], w[k + i], lo[i]);
+  }
+#pragma unroll
+  for (int k = 0; k < KA; ++k)
+#pragma unroll
+    for (int i = 0; i < L; ++i) acc[k] = madd<FMA>(acc[k], wd[k + i], hi[i]);
+}
+
+// Workgroup -> (signal, R-residue block, u-chunk)
+struct SweepGPos {
+  long long b;
+  int r0, u0, u1;
+};
+__device__ __forceinline__ bool sweepg_pos(long long B, int N, int h, int R, int uc, SweepGPos* w) {
+  const int nu = N / h, nrb = h / R, nch = (nu + uc - 1) / uc;
   long long id = blockIdx.x;
   const int ch = (int)(id % nch);
   id /= nch;
-  const int rb = (int)(id % nrb);
-  const long long b = id / nrb;
-  if (b >= p.B) return;  // workgroup-uniform
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int r = rb * 64 + lane;
-  const int u0 = ch * uc, u1 = min(u0 + uc, nu);
-  const int nblk = (u1 - u0 + KB - 1) / KB;
-  const size_t row = (size_t)b * (size_t)N;
-  auto wrap = [&](long long t) -> long long { return t >= N ? t - N : t; };
-  if (wave < 2) {
-    // ---- stage A: level j over parity class e (t = r + e*h + v*s), blocks 0 .. nblk
-    const int e = wave;
-    const T thr_b = p.thr ? p.thr[b] : T(0);
-    const T* sa = p.src_a ? p.src_a + row : nullptr;
-    const T* sd = (p.src_d && p.use_d) ? p.src_d + row : nullptr;
-    auto fa = [&](long long t) -> T { return sa ? sa[wrap(t)] : T(0); };
-    auto fd = [&](long long t) -> T {
-      if (!sd) return T(0);
-      const T v = sd[wrap(t)];
-      return p.thr ? threshold_t(v, thr_b, p.soft) : v;
-    };
-    SweepWin<T, L, KA, 1> A, D;
-    long long tb = (long long)r + (long long)e * h + (long long)(u0 >> 1) * s;
-    A.fill_head(tb, s, 0, fa);
-    D.fill_head(tb, s, 0, fd);
+  w->r0 = (int)(id % nrb) * R;
+  w->b = id / nrb;
+  w->u0 = ch * uc;
+  w->u1 = min(w->u0 + uc, nu);
+  return w->b < B;
+}
+
+// Top stage, class e of G: level-j sweep over t = r + e*h + v*G*h; one step writes KA outputs.
+template <typename T, int L, bool FMA, int KA>
+struct SweepTop {
+  SweepWin<T, L, KA, 1> A, D;
+  long long tb;
+  int S, N;
+  const T *sa, *sd;
+  bool thr_on;
+  T thr_b;
+  int soft;
+  __device__ __forceinline__ T fa(long long t) const { return sa ? sa[t >= N ? t - N : t] : T(0); }
+  __device__ __forceinline__ T fd(long long t) const {
+    if (!sd) return T(0);
+    const T v = sd[t >= N ? t - N : t];
+    return thr_on ? threshold_t(v, thr_b, soft) : v;
+  }
+  __device__ __forceinline__ void start() {
+    A.fill_head(tb, S, 0, [&](long long t) { return fa(t); });
+    D.fill_head(tb, S, 0, [&](long long t) { return fd(t); });
+  }
+  template <typename Out>
+  __device__ __forceinline__ void step(const T* lo, const T* hi, Out&& out) {
+    A.load_block(tb, S, 0, [&](long long t) { return fa(t); });
+    D.load_block(tb, S, 0, [&](long long t) { return fd(t); });
+#pragma unroll
+    for (int k = 0; k < KA; ++k) {
+      T acc = T(0);
+#pragma unroll
+      for (int i = 0; i < L; ++i) acc = madd<FMA>(acc, A.tap(k, i), lo[i]);
+#pragma unroll
+      for (int i = 0; i < L; ++i) acc = madd<FMA>(acc, D.tap(k, i), hi[i]);
+      out(k, acc);
+    }
+    A.shift();
+    D.shift();
+    tb += (long long)KA * S;
+  }
+};
+
+// Pair (G = 2): groups 0, 1 top (parity), 2, 3 bottom (half of a block).
+template <typename T, int L, bool FMA, int KA, int R>
+__global__ void __launch_bounds__(4 * R) k_inverse_sweep2(const LevelArgs<T> p) {
+  constexpr int KB = 2 * KA;
+  constexpr int RING = 3 * KB;
+  static_assert(KB >= L - 1, "the bottom level reads at most one block ahead");
+  __shared__ T ring[RING * R];
+  const int S = p.lv.s, h = S >> 1, N = p.N;
+  SweepGPos w;
+  if (!sweepg_pos(p.B, N, h, R, p.tile, &w)) return;  // workgroup-uniform
+  const int g = threadIdx.x / R, lane = threadIdx.x % R;
+  const int r = w.r0 + lane;
+  const int nblk = (w.u1 - w.u0 + KB - 1) / KB;
+  const size_t row = (size_t)w.b * (size_t)N;
+  if (g < 2) {
+    SweepTop<T, L, FMA, KA> top;
+    top.S = S; top.N = N; top.soft = p.soft;
+    top.sa = p.src_a ? p.src_a + row : nullptr;
+    top.sd = (p.src_d && p.use_d) ? p.src_d + row : nullptr;
+    top.thr_on = p.thr != nullptr;
+    top.thr_b = p.thr ? p.thr[w.b] : T(0);
+    top.tb = (long long)r + (long long)g * h + (long long)(w.u0 >> 1) * S;
+    top.start();
     for (int n = 0; n <= nblk + 1; ++n) {
       if (n <= nblk) {
-        A.load_block(tb, s, 0, fa);
-        D.load_block(tb, s, 0, fd);
-        T* rn = ring + (n % 3) * KB * 64 + e * 64 + lane;
-#pragma unroll
-        for (int k = 0; k < KA; ++k) {
-          T acc = T(0);
-#pragma unroll
-          for (int i = 0; i < L; ++i) acc = madd<FMA>(acc, A.tap(k, i), p.lo[i]);
-#pragma unroll
-          for (int i = 0; i < L; ++i) acc = madd<FMA>(acc, D.tap(k, i), p.hi[i]);
-          rn[2 * k * 64] = acc;  // u = u0 + n*KB + 2k + e
-        }
-        A.shift();
-        D.shift();
-        tb += (long long)KA * s;
+        T* rn = ring + ((n % 3) * KB + g) * R + lane;
+        top.step(p.lo, p.hi, [&](int k, T v) { rn[2 * k * R] = v; });  // u = u0 + n*KB + 2k + g
       }
       __syncthreads();
     }
   } else {
-    // ---- stage B: level j-1 over class r mod h, half hh of block n-2 at step n
-    const int hh = wave - 2;
-    const T thr_b = p.thr2 ? p.thr2[b] : T(0);
+    const int hh = g - 2;
     const T* sd = (p.src_d2 && p.use_d2) ? p.src_d2 + row : nullptr;
+    const T thr_b = p.thr2 ? p.thr2[w.b] : T(0);
     T* y = p.out_a + row;
     for (int n = 0; n <= nblk + 1; ++n) {
       if (n >= 2) {
         const int m = n - 2;
-        const int ub = u0 + m * KB + hh * KA;  // first output u of this half-block
-        const int sb = (m % 3) * KB + hh * KA;  // its ring slot
-        T w[KA + L - 1];
+        const int ub = w.u0 + m * KB + hh * KA;
         T acc[KA];
-        // d_{j-1} window first: its loads are in flight during the approximation branch
-        T wd[KA + L - 1];
+        sweep_ring_stage<T, L, FMA, KA, R, RING>(ring, lane, (m % 3) * KB + hh * KA, 1, sd, p.thr2 != nullptr, thr_b,
+                                                 p.soft, (long long)r + (long long)ub * h, h, N, p.lo, p.hi, acc);
 #pragma unroll
-        for (int x = 0; x < KA + L - 1; ++x) {
-          if (sd) {
-            const T v = sd[wrap((long long)r + (long long)(ub + x) * h)];
-            wd[x] = p.thr2 ? threshold_t(v, thr_b, p.soft) : v;
-          } else {
-            wd[x] = T(0);
-          }
-        }
+        for (int k = 0; k < KA; ++k)
+          if (ub + k < w.u1) y[(size_t)r + (size_t)(ub + k) * (size_t)h] = acc[k];
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// Triple (G = 4): groups 0..3 top (class u mod 4), 4..7 middle (parity, half), 8..11 bottom (quarter).
+template <typename T, int L, bool FMA, int KA, int R>
+__global__ void __launch_bounds__(12 * R) k_inverse_sweep3(const LevelArgs<T> p) {
+  constexpr int KB = 4 * KA;
+  constexpr int RING = 3 * KB;
+  static_assert(KB >= 2 * (L - 1), "the middle level reads at most one block ahead");
+  __shared__ T ring1[RING * R];
+  __shared__ T ring2[RING * R];
+  const int S = p.lv.s, h = S >> 2, N = p.N;
+  SweepGPos w;
+  if (!sweepg_pos(p.B, N, h, R, p.tile, &w)) return;  // workgroup-uniform
+  const int g = threadIdx.x / R, lane = threadIdx.x % R;
+  const int r = w.r0 + lane;
+  const int nblk = (w.u1 - w.u0 + KB - 1) / KB;
+  const size_t row = (size_t)w.b * (size_t)N;
+  // top: blocks 0 .. nblk+1 at steps n; middle: blocks 0 .. nblk at n-2; bottom: blocks 0 .. nblk-1 at n-4
+  if (g < 4) {
+    SweepTop<T, L, FMA, KA> top;
+    top.S = S; top.N = N; top.soft = p.soft;
+    top.sa = p.src_a ? p.src_a + row : nullptr;
+    top.sd = (p.src_d && p.use_d) ? p.src_d + row : nullptr;
+    top.thr_on = p.thr != nullptr;
+    top.thr_b = p.thr ? p.thr[w.b] : T(0);
+    top.tb = (long long)r + (long long)g * h + (long long)(w.u0 >> 2) * S;
+    top.start();
+    for (int n = 0; n <= nblk + 3; ++n) {
+      if (n <= nblk + 1) {
+        T* rn = ring1 + ((n % 3) * KB + g) * R + lane;
+        top.step(p.lo, p.hi, [&](int k, T v) { rn[4 * k * R] = v; });  // u = u0 + n*KB + 4k + g
+      }
+      __syncthreads();
+    }
+  } else if (g < 8) {
+    const int e2 = (g - 4) & 1, half = (g - 4) >> 1;
+    const T* sd = (p.src_d2 && p.use_d2) ? p.src_d2 + row : nullptr;
+    const T thr_b = p.thr2 ? p.thr2[w.b] : T(0);
+    for (int n = 0; n <= nblk + 3; ++n) {
+      if (n >= 2 && n <= nblk + 2) {
+        const int m = n - 2;
+        const int o = e2 + 2 * half * KA;  // u offset of this group's first output in the block
+        const int ub = w.u0 + m * KB + o;
+        T acc[KA];
+        sweep_ring_stage<T, L, FMA, KA, R, RING>(ring1, lane, (m % 3) * KB + o, 2, sd, p.thr2 != nullptr, thr_b, p.soft,
+                                                 (long long)r + (long long)ub * h, 2LL * h, N, p.lo, p.hi, acc);
+        T* rn = ring2 + ((m % 3) * KB + o) * R + lane;
 #pragma unroll
-        for (int x = 0; x < KA + L - 1; ++x) {
-          const int sl = sb + x;
-          w[x] = ring[(sl >= RING ? sl - RING : sl) * 64 + lane];
-        }
+        for (int k = 0; k < KA; ++k) rn[2 * k * R] = acc[k];
+      }
+      __syncthreads();
+    }
+  } else {
+    const int q = g - 8;
+    const T* sd = (p.src_d3 && p.use_d3) ? p.src_d3 + row : nullptr;
+    const T thr_b = p.thr3 ? p.thr3[w.b] : T(0);
+    T* y = p.out_a + row;
+    for (int n = 0; n <= nblk + 3; ++n) {
+      if (n >= 4) {
+        const int m = n - 4;
+        const int ub = w.u0 + m * KB + q * KA;
+        T acc[KA];
+        sweep_ring_stage<T, L, FMA, KA, R, RING>(ring2, lane, (m % 3) * KB + q * KA, 1, sd, p.thr3 != nullptr, thr_b,
+                                                 p.soft, (long long)r + (long long)ub * h, h, N, p.lo, p.hi, acc);
 #pragma unroll
-        for (int k = 0; k < KA; ++k) {
-          acc[k] = T(0);
-#pragma unroll
-          for (int i = 0; i < L; ++i) acc[k] = madd<FMA>(acc[k], w[k + i], p.lo[i]);
-        }
-#pragma unroll
-        for (int k = 0; k < KA; ++k) {
-#pragma unroll
-          for (int i = 0; i < L; ++i) acc[k] = madd<FMA>(acc[k], wd[k + i], p.hi[i]);
-          if (ub + k < u1) y[(size_t)r + (size_t)(ub + k) * (size_t)h] = acc[k];
-        }
+        for (int k = 0; k < KA; ++k)
+          if (ub + k < w.u1) y[(size_t)r + (size_t)(ub + k) * (size_t)h] = acc[k];
       }
       __syncthreads();
     }

@@ -102,9 +102,12 @@ struct LevelArgs {
   const T* src_a;       // forward: level input [B][lda]; inverse: approx input [B][N]
   long long lda;
   const T* src_d;       // inverse: details of this level [B][N]
-  const T* src_d2;      // k_inverse_sweep2: details of level j-1 [B][N]
-  const T* thr2;        // k_inverse_sweep2: thresholds of level j-1
+  const T* src_d2;      // k_inverse_sweep2/3: details of level j-1 [B][N]
+  const T* thr2;        // k_inverse_sweep2/3: thresholds of level j-1
   int use_d2;
+  const T* src_d3;      // k_inverse_sweep3: details / thresholds of level j-2
+  const T* thr3;
+  int use_d3;
   T* out_a;             // forward: approx out [B][N]; inverse: y out [B][N]
   T* out_d;             // forward: detail out [B][N]
   const T* hist;        // kHaloHistory source [B][hist_len]
@@ -190,7 +193,7 @@ hipError_t launch_forward_sweep(const LevelArgs<T>& a, bool fma, hipStream_t st)
 template <typename T>
 hipError_t launch_inverse_sweep(const LevelArgs<T>& a, bool fma, hipStream_t st);
 template <typename T>
-hipError_t launch_inverse_sweep2(const LevelArgs<T>& a, int ka, bool fma, hipStream_t st);
+hipError_t launch_inverse_sweepg(const LevelArgs<T>& a, int levels, int ka, int R, bool fma, hipStream_t st);
 template <typename T>
 hipError_t launch_forward_multi(const MultiArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
 template <typename T>

@@ -81,31 +81,47 @@ hipError_t launch_inverse_sweep(const LevelArgs<T>& a, bool fma, hipStream_t st)
 template hipError_t launch_forward_sweep<VW_T>(const LevelArgs<VW_T>&, bool, hipStream_t);
 template hipError_t launch_inverse_sweep<VW_T>(const LevelArgs<VW_T>&, bool, hipStream_t);
 
-// Two inverse levels per launch (k_inverse_sweep2): one workgroup per (signal, 64-residue block,
-// u-chunk).  KA = 8 or 16 outputs per stage-A thread and step.
-template <typename T, int L, bool FMA, int KA>
-static hipError_t run_inverse_sweep2(const LevelArgs<T>& a, hipStream_t st) {
-  const long long h = a.lv.s / 2, nu = a.N / h, nch = (nu + a.tile - 1) / a.tile;
-  const long long groups = a.B * (h / 64) * nch;
-  hipLaunchKernelGGL((k_inverse_sweep2<T, L, FMA, KA>), dim3((unsigned)groups), dim3(kSweep2Threads), 0, st, a);
-  return hipGetLastError();
+// Two / three inverse levels per launch (k_inverse_sweep2 / k_inverse_sweep3): one workgroup per (signal,
+// R-residue block, u-chunk) of 4R / 12R threads.  KA = 8 or 16 outputs per thread and step; a block
+// (G*KA positions) must cover the reach of the levels below the top, and the rings must fit LDS
+// (the host applies the same rule: vw_capi.cpp sweepg_plan).
+template <typename T, int L, bool FMA, int KA, int R, int G>
+static hipError_t run_inverse_sweepg(const LevelArgs<T>& a, hipStream_t st) {
+  constexpr int KMIN = (G == 2 ? 1 : 2) * (L - 1);
+  constexpr bool fits = (G == 2 ? 1 : 2) * 3 * G * KA * R * (int)sizeof(T) <= kLdsBytes;
+  if constexpr (G * KA >= KMIN && fits) {
+    const long long h = a.lv.s / G, nu = a.N / h, nch = (nu + a.tile - 1) / a.tile;
+    const long long groups = a.B * (h / R) * nch;
+    if constexpr (G == 2)
+      hipLaunchKernelGGL((k_inverse_sweep2<T, L, FMA, KA, R>), dim3((unsigned)groups), dim3(4 * R), 0, st, a);
+    else
+      hipLaunchKernelGGL((k_inverse_sweep3<T, L, FMA, KA, R>), dim3((unsigned)groups), dim3(12 * R), 0, st, a);
+    return hipGetLastError();
+  } else {
+    return hipErrorInvalidValue;
+  }
+}
+
+template <typename T, int L, bool FMA, int G>
+static hipError_t run_inverse_sweepg_k(const LevelArgs<T>& a, int ka, int R, hipStream_t st) {
+  if (ka == 8) return R == 64 ? run_inverse_sweepg<T, L, FMA, 8, 64, G>(a, st) : run_inverse_sweepg<T, L, FMA, 8, 32, G>(a, st);
+  return R == 64 ? run_inverse_sweepg<T, L, FMA, 16, 64, G>(a, st) : run_inverse_sweepg<T, L, FMA, 16, 32, G>(a, st);
 }
 
 template <typename T>
-hipError_t launch_inverse_sweep2(const LevelArgs<T>& a, int ka, bool fma, hipStream_t st) {
+hipError_t launch_inverse_sweepg(const LevelArgs<T>& a, int levels, int ka, int R, bool fma, hipStream_t st) {
+  if (R != 64 && R != 32) return hipErrorInvalidValue;
   switch (a.taps) {
-#define VW_CASE(n)                                                                                  \
-    case n:                                                                                         \
-      if constexpr (n <= 17) {                                                                      \
-        if (ka == 8) return fma ? run_inverse_sweep2<T, n, true, 8>(a, st) : run_inverse_sweep2<T, n, false, 8>(a, st); \
-      }                                                                                             \
-      return fma ? run_inverse_sweep2<T, n, true, 16>(a, st) : run_inverse_sweep2<T, n, false, 16>(a, st);
+#define VW_CASE(n)                                                                                   \
+    case n:                                                                                          \
+      if (levels == 2) return fma ? run_inverse_sweepg_k<T, n, true, 2>(a, ka, R, st) : run_inverse_sweepg_k<T, n, false, 2>(a, ka, R, st); \
+      return fma ? run_inverse_sweepg_k<T, n, true, 4>(a, ka, R, st) : run_inverse_sweepg_k<T, n, false, 4>(a, ka, R, st);
     VW_TAP_LIST(VW_CASE)
 #undef VW_CASE
     default: return hipErrorInvalidValue;
   }
 }
-template hipError_t launch_inverse_sweep2<VW_T>(const LevelArgs<VW_T>&, int, bool, hipStream_t);
+template hipError_t launch_inverse_sweepg<VW_T>(const LevelArgs<VW_T>&, int, int, int, bool, hipStream_t);
 
 template <typename T>
 hipError_t launch_forward_level(const LevelArgs<T>& a, int lds, bool fma, hipStream_t st) {
