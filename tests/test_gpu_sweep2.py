@@ -17,6 +17,15 @@ from vectorwave_amd.wavelets import Coiflet, Daubechies, Haar, Symlet
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def short_classes(engine):
+    """The small shapes here have short residue classes, which the default policy leaves to one sweep per
+    level (VW_SWEEP2_MINB = 64 blocks): admit them so the kernels' edge cases run at test sizes."""
+    engine.set_option("VW_SWEEP2_MINB", 1)
+    yield
+    engine.set_option("VW_SWEEP2_MINB", -1)
+
+
 def _rows(B, n, seed):
     return np.stack([O.java_random_signal(n, seed + b) for b in range(B)])
 
@@ -91,3 +100,15 @@ def test_pair_denoise_thresholds(engine):
         y_ref, t_ref = O.swt_denoise(x[b], *lohi(w), O.PERIODIC, J, wavelet_id=w.wavelet_id)
         assert thr[b] == t_ref
         assert np.array_equal(y[b], y_ref)
+
+
+def test_default_policy_triple_on_long_blocks(engine):
+    """The default policy (VW_SWEEP2_MINB = 64) on a 2^18-sample db8 block: levels (10,9,8) as a triple of
+    64-residue groups, (7,6) as a pair of 32-residue groups; bit-exact against the restatement."""
+    w = Daubechies.DB8
+    n, J = 1 << 18, 10
+    x = _rows(1, n, 3)
+    d, a = engine.forward(x, *lohi(w), w.wavelet_id, O.PERIODIC, J, 0)
+    with engine.options(VW_SWEEP2_MINB=-1):
+        y = engine.inverse(d, a, *lohi_r(w), w.wavelet_id, O.PERIODIC, J, 0)
+    assert np.array_equal(y[0], O.reconstruct(d[:, 0, :], a[0], *lohi_r(w), O.PERIODIC))

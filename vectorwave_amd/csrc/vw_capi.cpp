@@ -99,6 +99,7 @@ struct Tuning {
   int sweep2_ka = 8;           // VW_SWEEP2_KA: stage-A outputs per thread and step (8 or 16)
   int sweep2_uc = 2048;        // VW_SWEEP2_UC: u positions per workgroup chunk (512 / 1024 / 2048: 9.68 / 9.50 / 9.33 ms db8 inverse)
   int sweep2_r = 0;            // VW_SWEEP2_R=32: 32-residue groups even where h allows 64 (0 = widest)
+  int sweep2_minb = 64;        // VW_SWEEP2_MINB: blocks a residue class needs for the chained sweeps
   int blk_fwd8 = 0;            // VW_BLK_FWD8=1: register-blocked forward at NV = 8 (1024-thread workgroups)
 };
 
@@ -139,6 +140,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_SWEEP2_KA") t.sweep2_ka = v == 16 ? 16 : v == 8 ? 8 : d.sweep2_ka;
   else if (k == "VW_SWEEP2_UC") t.sweep2_uc = v >= 32 ? v : d.sweep2_uc;
   else if (k == "VW_SWEEP2_R") t.sweep2_r = v == 32 ? 32 : 0;
+  else if (k == "VW_SWEEP2_MINB") t.sweep2_minb = v < 0 ? d.sweep2_minb : v;
   else if (k == "VW_BLK_FWD8") t.blk_fwd8 = v < 0 ? d.blk_fwd8 : v;
   else return false;
   return true;
@@ -149,7 +151,7 @@ static const char* const kTuningKeys[] = {
     "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_MULTI_PF", "VW_MULTI_PAD", "VW_MULTI_INV_TILE", "VW_NO_SWEEP", "VW_SWEEP_QC",
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
-    "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_BLK_FWD8"};
+    "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -845,7 +847,7 @@ static std::vector<int> level_groups(const Tuning& tu, const std::vector<LevelDe
 // groups, PERIODIC / dir +1 / offset 0.  Picks KA (outputs per thread and step) and R (residues per
 // group, 64 or 32 = h's alignment) under the kernels' rules: a block of G*KA positions covers the
 // reach of the levels below the top (L-1 per level, in the bottom level's positions: 1 / 2 steps), the
-// LDS rings (1 / 2 of 3 blocks x R) fit, and one wrap mod N at most.
+// LDS rings (1 / 2 of 3 blocks x R) fit, one wrap mod N at most, and residue classes of >= 64 blocks.
 template <typename T>
 static bool sweepg_plan(const Tuning& tu, const std::vector<LevelDesc>& lv, int j, int levels, int L, int64_t N,
                         const std::vector<char>& in_group, const std::vector<int>& start_of, int* ka_out, int* r_out) {
@@ -866,6 +868,10 @@ static bool sweepg_plan(const Tuning& tu, const std::vector<LevelDesc>& lv, int 
       const int64_t lds = (levels == 2 ? 1 : 2) * 3 * kb * r * (int64_t)sizeof(T);
       if (kb < kmin || lds > kLdsBytes || h % r != 0) continue;
       if (N % (G * h) != 0 || (2 * kb + 2 * L) * G * h > N) continue;
+      // short residue classes: the pipeline's fill (2 / 4 steps per chunk) is not amortised -- on sym8
+      // 16384-sample signals through the tiled path a triple ran 21.2 ms vs 12.3 for pairs
+      // (profiles/r03/ab_sweepg_short.log); such levels keep one sweep each
+      if (N / h < (int64_t)tu.sweep2_minb * kb) continue;
       *ka_out = ka;
       *r_out = r;
       return true;
