@@ -1268,6 +1268,51 @@ __device__ __forceinline__ void blk_fwd(const T* X, const BlkLayout& lo, int HLV
     }
 }
 
+// blk_fwd with wave-uniform offsets (as blk_inv_branch_s): Xb = X + blk_phys(layout, vb + HLV) * V, and the
+// read of logical vector vb + HLV + q*m sits off(q) = q*m + ((q*m) >> sh)*pad from it for every thread
+// when the pad groups align with a thread's block and HLV is a multiple of the group (host: vw_capi.cpp
+// rounds HLV up to 16 vectors); q*m < 0 shifts arithmetically (floor), as blk_phys does.
+template <typename T, int L, bool FMA, int NV>
+__device__ __forceinline__ void blk_fwd_s(const T* Xb, int m, int sh, int pad, const T* flo, const T* fhi,
+                                          T (&al)[NV][VT<T>::V], T (&ah)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  constexpr int TC = blk_chunk<T, NV>();
+#pragma unroll
+  for (int r = 0; r < NV; ++r)
+#pragma unroll
+    for (int e = 0; e < V; ++e) { al[r][e] = T(0); ah[r][e] = T(0); }
+  static_for<0, (L + TC - 1) / TC>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * TC;
+    constexpr int I1 = (I0 + TC < L) ? I0 + TC : L;
+    T fl[I1 - I0], fh[I1 - I0];
+#pragma unroll
+    for (int i = I0; i < I1; ++i) { fl[i - I0] = flo[i]; fh[i - I0] = fhi[i]; }
+#pragma unroll
+    for (int q = NV - 1 - I0; q > -I1; --q) {
+      const int qm = __builtin_amdgcn_readfirstlane(q * m);
+      const int off = __builtin_amdgcn_readfirstlane(qm + (qm >> sh) * pad);
+      const vec x = *reinterpret_cast<const vec*>(Xb + off * V);
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        const int i = r - q;
+        if (i >= I0 && i < I1) {
+          vmadd<FMA, kPkFwd>(al[r], x, fl[i - I0]);
+          vmadd<FMA, kPkFwd>(ah[r], x, fh[i - I0]);
+        }
+      }
+      if (((NV - 1 - I0 - q) & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+#pragma unroll
+  for (int r = 0; r < NV; ++r)
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      asm volatile("" : "+v"(al[r][e]));
+      asm volatile("" : "+v"(ah[r][e]));
+    }
+}
+
 // Forward, PERIODIC, one signal per workgroup: MultiLevelMODWTTransform.decompose (:243-251) /
 // BatchSIMDMODWT.batchMultiLevelMODWTSoA (:362-377) / VectorWaveSwtAdapter forward.  Level inputs in
 // one LDS buffer (p.region1 == 0: two barriers per level) or two (one barrier).  Left wrap images:
@@ -1326,7 +1371,12 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
     int vb = 0;
     if (m) {
       vb = blk_base<NV>(m);
-      blk_fwd<T, L, FMA, NV>(X, blk_layout(m, NV, p.blk_tight), HLV, vb, m, flo, fhi, al, ah);
+      const BlkLayout lo = blk_layout(m, NV, p.blk_tight);
+      const int sh = __builtin_amdgcn_readfirstlane(lo.sh), pad = __builtin_amdgcn_readfirstlane(lo.pad);
+      if (VW_BLK_SOFF && NV >= 8 && (pad == 0 || (((m * NV) & ((1 << sh) - 1)) == 0 && (HLV & ((1 << sh) - 1)) == 0)))
+        blk_fwd_s<T, L, FMA, NV>(X + blk_phys(lo, vb + HLV) * V, m, sh, pad, flo, fhi, al, ah);
+      else
+        blk_fwd<T, L, FMA, NV>(X, lo, HLV, vb, m, flo, fhi, al, ah);
       if (m < VW_BLK_NT_M) {
         // a lane's outputs are m*16-byte pieces NV*m*16 bytes apart: write-back stores, so that L2
         // merges a line's pieces before it goes to HBM (nontemporal stores of 16-byte pieces wrote

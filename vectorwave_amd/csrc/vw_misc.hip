@@ -46,18 +46,21 @@ hipError_t launch_history_update(const T* in, long long ld_in, const T* old_hist
   return hipGetLastError();
 }
 
+static hipError_t run_sigma(const double* x, long long ld, long long B, int N, double scale_c, double* sigma_out,
+                            double* thr_out, const double* center, double* median_out, hipStream_t st) {
+  hipLaunchKernelGGL(k_noise_sigma, dim3((unsigned)B), dim3(kSigmaThreads), 0, st, x, ld, N, scale_c, sigma_out,
+                     thr_out, center, median_out);
+  return hipGetLastError();
+}
+
 hipError_t launch_noise_sigma(const double* coeffs, long long ld, long long B, int N, double scale_c,
                               double* sigma_out, double* thr_out, hipStream_t st) {
-  hipLaunchKernelGGL(k_noise_sigma, dim3((unsigned)B), dim3(kSigmaThreads), 0, st, coeffs, ld, N, scale_c, sigma_out,
-                     thr_out, (const double*)nullptr, (double*)nullptr);
-  return hipGetLastError();
+  return run_sigma(coeffs, ld, B, N, scale_c, sigma_out, thr_out, (const double*)nullptr, (double*)nullptr, st);
 }
 
 hipError_t launch_median(const double* x, long long ld, long long B, int N, const double* center, double* median_out,
                          hipStream_t st) {
-  hipLaunchKernelGGL(k_noise_sigma, dim3((unsigned)B), dim3(kSigmaThreads), 0, st, x, ld, N, 0.0, (double*)nullptr,
-                     (double*)nullptr, center, median_out);
-  return hipGetLastError();
+  return run_sigma(x, ld, B, N, 0.0, (double*)nullptr, (double*)nullptr, center, median_out, st);
 }
 
 __global__ void __launch_bounds__(256) k_abs_center(const double* __restrict__ x, long long ld, int N,

@@ -33,7 +33,7 @@ __device__ __forceinline__ void radix_median(const double* __restrict__ c, int N
   }
   for (int shift = 56; shift >= 0; shift -= 8) {
     for (int q = tid; q < 512; q += kSigmaThreads) hist[q >> 8][q & 255] = 0u;
-    __syncthreads();
+    lds_barrier();
     const unsigned long long hm = (shift == 56) ? 0ull : (~0ull << (shift + 8));
     const unsigned long long p0 = prefix[0], p1 = prefix[1];
     if (in_regs) {
@@ -55,7 +55,7 @@ __device__ __forceinline__ void radix_median(const double* __restrict__ c, int N
         if (nsel == 2 && ((key ^ p1) & hm) == 0) atomicAdd(&hist[1][d], 1u);
       }
     }
-    __syncthreads();
+    lds_barrier();
     // exclusive scan of 2 x 256 bins by threads 0..511 (wave-level shuffles)
     const int r = tid >> 8, bin = tid & 255, lane = tid & 63, wv = (tid >> 6) & 3;
     unsigned incl = 0;
@@ -69,7 +69,7 @@ __device__ __forceinline__ void radix_median(const double* __restrict__ c, int N
       }
       if (lane == 63) wsum[r][wv] = incl;
     }
-    __syncthreads();
+    lds_barrier();
     if (tid < 512 && r < nsel) {
       unsigned base = 0;
       for (int q = 0; q < wv; ++q) base += wsum[r][q];
@@ -81,7 +81,7 @@ __device__ __forceinline__ void radix_median(const double* __restrict__ c, int N
         krem[r] = k - (long long)excl;
       }
     }
-    __syncthreads();
+    lds_barrier();
   }
   *v1_out = __longlong_as_double((long long)prefix[0]);
   *v2_out = __longlong_as_double((long long)prefix[1]);
@@ -94,9 +94,9 @@ __device__ __forceinline__ double block_minmax(double v, bool is_max, double* re
     const double t = __shfl_xor(v, o, 64);
     v = is_max ? (t > v ? t : v) : (t < v ? t : v);
   }
-  __syncthreads();  // red[] free (previous use complete)
+  lds_barrier();  // red[] free (previous use complete)
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
+  lds_barrier();
   double r = red[0];
 #pragma unroll
   for (int q = 1; q < kSigmaThreads / 64; ++q) r = is_max ? (red[q] > r ? red[q] : r) : (red[q] < r ? red[q] : r);
@@ -116,9 +116,13 @@ constexpr int kSelCand = 1024;  // a bucket this small is finished by exact rank
 // spread-out digit, instead of eight radix passes whose first digits every key shares.
 // center (optional, [B]): the keys are |c - center[b]| (MathUtils.medianAbsoluteDeviation's second
 // pass; N <= 16384, keys in registers); median_out (optional): the raw median.
-__global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __restrict__ coeffs, long long ld, int N,
-                                                               double scale_c, double* sigma_out, double* thr_out,
-                                                               const double* __restrict__ center, double* median_out) {
+// One row b: keys from ck, fallback re-reads from c (both the row in HBM).  The barriers wait for LDS only
+// (lds_barrier): nothing here reads global memory a barrier must order.  (A persistent form that copied the
+// next row into LDS by DMA during the selection measured slower: profiles/r03/ab_sigma_pf_blkfwd8.log.)
+__device__ __forceinline__ void noise_sigma_row(long long b, const double* __restrict__ c, const double* ck, bool vec,
+                                                int N, double scale_c, double* sigma_out, double* thr_out,
+                                                const double* __restrict__ center, double* median_out) {
+  __shared__ int bad_any;
   __shared__ unsigned int hist[kSelBins];
   __shared__ double cand[kSelCand];
   __shared__ double red[kSigmaThreads / 64];
@@ -126,8 +130,6 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
   __shared__ long long sel[2][3];  // per rank: bucket, exclusive count, count
   __shared__ double res[2];
   __shared__ int ncand;
-  const long long b = blockIdx.x;
-  const double* c = coeffs + b * ld;
   const int tid = threadIdx.x;
   const bool in_regs = N <= kSigmaThreads * kSigmaKeys;
   const double ctr = center ? center[b] : 0.0;
@@ -137,13 +139,12 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
   double v1 = 0.0, v2 = 0.0;
   bool done = false;
   if (in_regs) {
-    const bool vec = (N % 2 == 0) && (ld % 2 == 0) && ((reinterpret_cast<uintptr_t>(coeffs) & 15) == 0);
     if (vec) {
       typedef double d2 __attribute__((ext_vector_type(2)));
 #pragma unroll
       for (int k = 0; k < kSigmaKeys / 2; ++k) {
         const int w = min(tid + k * kSigmaThreads, N / 2 - 1);
-        const d2 v = __builtin_nontemporal_load(reinterpret_cast<const d2*>(c) + w);
+        const d2 v = __builtin_nontemporal_load(reinterpret_cast<const d2*>(ck) + w);
         keys[2 * k] = key_of(v[0]);
         keys[2 * k + 1] = key_of(v[1]);
       }
@@ -151,8 +152,8 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
 #pragma unroll
       for (int k = 0; k < kSigmaKeys / 2; ++k) {
         const int i = 2 * (tid + k * kSigmaThreads);
-        keys[2 * k] = i < N ? key_of(c[i]) : 0ull;
-        keys[2 * k + 1] = i + 1 < N ? key_of(c[i + 1]) : 0ull;
+        keys[2 * k] = i < N ? key_of(ck[i]) : 0ull;
+        keys[2 * k + 1] = i + 1 < N ? key_of(ck[i + 1]) : 0ull;
       }
     }
     // key slot 2k+e holds element 2*(tid + k*1024) + e
@@ -169,7 +170,11 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
         hi = v > hi ? v : hi;
       }
     }
-    bad = __syncthreads_or(bad);
+    if (tid == 0) bad_any = 0;
+    lds_barrier();  // bad_any cleared
+    if (bad) bad_any = 1;
+    lds_barrier();
+    bad = bad_any != 0;
     lo = block_minmax(lo, false, red);
     hi = block_minmax(hi, true, red);
     long long r1 = k1, r2 = k2;  // ranks within the active keys [lo, hi]
@@ -179,13 +184,13 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
       if (!__builtin_isfinite(scale)) break;
       auto bucket = [&](double v) { return min(kSelBins - 1, (int)((v - lo) * scale)); };
       for (int q = tid; q < kSelBins; q += kSigmaThreads) hist[q] = 0u;
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int q = 0; q < kSigmaKeys; ++q) {
         const double v = val(q);
         if (valid(q) && v >= lo && v <= hi) atomicAdd(&hist[bucket(v)], 1u);
       }
-      __syncthreads();
+      lds_barrier();
       // scan: thread t owns bins 2t, 2t+1
       const unsigned h0 = hist[2 * tid], h1 = hist[2 * tid + 1];
       unsigned incl = h0 + h1;
@@ -196,7 +201,7 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
         if (lane >= o) incl += t;
       }
       if (lane == 63) wsum[wv] = incl;
-      __syncthreads();
+      lds_barrier();
       unsigned base = 0;
       for (int q = 0; q < wv; ++q) base += wsum[q];
       const long long e0 = (long long)(base + incl - h0 - h1), e1 = e0 + h0;
@@ -207,7 +212,7 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
         if (e1 <= rk && rk < e1 + h1) { sel[r][0] = 2 * tid + 1; sel[r][1] = e1; sel[r][2] = h1; }
       }
       if (tid == 0) ncand = 0;
-      __syncthreads();
+      lds_barrier();
       const int b1 = (int)sel[0][0], b2 = (int)sel[1][0];
       const long long ex1 = sel[0][1], cnt1 = sel[0][2];
       auto in_bucket = [&](int q, int bk) {
@@ -231,7 +236,7 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
 #pragma unroll
         for (int q = 0; q < kSigmaKeys; ++q)
           if (in_bucket(q, b1)) cand[atomicAdd(&ncand, 1)] = val(q);
-        __syncthreads();
+        lds_barrier();
         const int n = ncand;
         if (tid < n) {
           const double x = cand[tid];
@@ -244,7 +249,7 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
           if (lt <= r1 - ex1 && r1 - ex1 < le) res[0] = x;
           if (lt <= r2 - ex1 && r2 - ex1 < le) res[1] = x;
         }
-        __syncthreads();
+        lds_barrier();
         v1 = res[0];
         v2 = res[1];
         done = true;
@@ -283,6 +288,15 @@ __global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __r
     if (thr_out) thr_out[b] = sigma * scale_c;
     if (median_out) median_out[b] = median;
   }
+}
+
+__global__ void __launch_bounds__(kSigmaThreads) k_noise_sigma(const double* __restrict__ coeffs, long long ld, int N,
+                                                               double scale_c, double* sigma_out, double* thr_out,
+                                                               const double* __restrict__ center, double* median_out) {
+  const long long b = blockIdx.x;
+  const double* c = coeffs + b * ld;
+  const bool vec = (N % 2 == 0) && (ld % 2 == 0) && ((reinterpret_cast<uintptr_t>(coeffs) & 15) == 0);
+  noise_sigma_row(b, c, c, vec, N, scale_c, sigma_out, thr_out, center, median_out);
 }
 
 // MathUtils.standardDeviation (core/util/MathUtils.java:233-257): sequential sum -> mean, sequential
