@@ -19,9 +19,10 @@ import os
 import sys
 
 MEMBERS = {
-    "forward": ("k_forward_fused", "k_forward_persist", "k_forward_blk", "k_forward_level", "k_forward_multi", "k_forward_sweep"),
+    "forward": ("k_forward_fused", "k_forward_persist", "k_forward_blk", "k_forward_level", "k_forward_multi", "k_forward_sweep",
+                "k_forward_deep"),
     "inverse": ("k_inverse_fused", "k_inverse_seq", "k_inverse_db", "k_inverse_blk", "k_inverse_level", "k_inverse_multi",
-                "k_inverse_sweep"),
+                "k_inverse_sweep", "k_inverse_sweep2", "k_inverse_sweep3", "k_inverse_deep"),
     "sigma": ("k_noise_sigma",),
 }
 
