@@ -31,10 +31,12 @@ namespace vw {
 constexpr int kDeepNP = 2;                // positions per thread
 constexpr int kDeepT = 64 * kDeepNP;      // decimated positions per tile (256 threads = 64 x 4 chunks)
 
-// Global stores of the deep kernels (experiment builds: -DVW_DEEP_STORE=0 none, 2 plain; default 1
-// non-temporal)
+// Global stores of the deep kernels (experiment builds: -DVW_DEEP_STORE=0 none, 1 non-temporal).  Default
+// 2, plain write-back stores: four residue-block workgroups write 64-byte pieces of each 256-byte span, and
+// L2 merges a line's pieces before it goes to HBM (non-temporal: 7.0 rows written for 6 on db8-stream;
+// write-back forward 8.70-8.74 vs 8.80-8.84 ms, profiles/r03/ab_deep_store_db8.log)
 #ifndef VW_DEEP_STORE
-#define VW_DEEP_STORE 1
+#define VW_DEEP_STORE 2
 #endif
 template <typename vec, typename T>
 __device__ __forceinline__ void deep_store(T* dst, const vec& v) {
