@@ -87,6 +87,10 @@ def parse(argv=None):
                    help="HIP events around every kernel launch inside the timed steps (inline) or none")
     p.add_argument("--contexts", type=int, default=0,
                    help="contexts (each on its own stream) sharing a GPU's rows; 0 = policy (see run())")
+    p.add_argument("--rotate", type=int, default=1,
+                   help="R buffer sets, step i reading set i mod R (R * input bytes beyond the 256 MiB Infinity "
+                        "Cache: no step re-reads what an earlier one left on die); 1 = one set")
+    p.add_argument("--rotate-outputs", action="store_true", help="--rotate also the output buffers")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--dry-run", action="store_true",
@@ -281,52 +285,88 @@ def dry_run(args, world, rank):
 
 
 class Part:
-    """One context's share of a rank's rows: its own vw_ctx, torch stream and buffers."""
+    """One context's share of a rank's rows: its own vw_ctx, torch stream and buffers.
 
-    def __init__(self, eng, stream, w, J, rows, N, dtype, pipeline, row_offset, torch):
+    `rotate` R > 1 keeps R input buffers (and, with `rotate_outputs`, R output sets) and step i uses set
+    i mod R, so a buffer is re-read only after R steps of other traffic: with R * rows * N * size beyond
+    the 256 MiB Infinity Cache no step can be served from what an earlier step left on die
+    (VERDICT r3 #1; `--rotate`).  Every set holds the same input values (same generator offset)."""
+
+    def __init__(self, eng, stream, w, J, rows, N, dtype, pipeline, row_offset, torch, rotate=1,
+                 rotate_outputs=False):
         from vectorwave_amd import _native as nat
         self.nat, self.eng, self.lib, self.stream = nat, eng, eng.lib, stream
         self.w, self.J, self.rows, self.N, self.pipeline = w, J, rows, N, pipeline
         self.f32 = dtype == "f32"
         tdt = torch.float32 if self.f32 else torch.float64
         dev = torch.device("cuda", eng.device)
+        self.rotate = max(1, rotate)
+        nout = self.rotate if rotate_outputs else 1
+        self.sets = []
         with torch.cuda.stream(stream):
-            self.x = torch.empty((rows, N), dtype=tdt, device=dev)
-            eng.fill_uniform(self.x, 42, offset=row_offset * N)
-            self.y = torch.empty((rows, N), dtype=tdt, device=dev)
-            if pipeline == "fwd+inv":
-                self.det = torch.empty((J, rows, N), dtype=tdt, device=dev)
-                self.app = torch.empty((rows, N), dtype=tdt, device=dev)
-            else:
-                self.thr = torch.empty((rows,), dtype=torch.float64, device=dev)
+            for r in range(self.rotate):
+                st = {"x": torch.empty((rows, N), dtype=tdt, device=dev)}
+                eng.fill_uniform(st["x"], 42, offset=row_offset * N)
+                if r < nout:
+                    st["y"] = torch.empty((rows, N), dtype=tdt, device=dev)
+                    if pipeline == "fwd+inv":
+                        st["det"] = torch.empty((J, rows, N), dtype=tdt, device=dev)
+                        st["app"] = torch.empty((rows, N), dtype=tdt, device=dev)
+                    else:
+                        st["thr"] = torch.empty((rows,), dtype=torch.float64, device=dev)
+                else:
+                    st.update({k: v for k, v in self.sets[0].items() if k != "x"})
+                self.sets.append(st)
             eng.bind_torch_stream()
+        self.last = 0   # the set the most recent step used (verify() checks that one)
         lo, hi = w.lowPassDecomposition(), w.highPassDecomposition()
         self.L = len(lo)
         self.lo_a, self.hi_a = nat.taps_array(lo), nat.taps_array(hi)
+
+    def __getattr__(self, k):  # x / y / det / app / thr of the most recently used set
+        if k in ("x", "y", "det", "app", "thr"):
+            return self.__dict__["sets"][self.__dict__["last"]][k]
+        raise AttributeError(k)
+
+    def footprint(self):
+        seen, tot = set(), 0
+        for st in self.sets:
+            for t in st.values():
+                if t.data_ptr() not in seen:
+                    seen.add(t.data_ptr())
+                    tot += t.numel() * t.element_size()
+        return tot
 
     def _check(self, st):
         if st != 0:
             raise RuntimeError(f"engine status {st}: {self.nat.last_error()}")
 
     def step_fn(self, flags):
-        """One step of this part: the config's passes over its rows, as C-ABI calls on its context."""
+        """One step of this part: the config's passes over its rows, as C-ABI calls on its context.
+        Returns step(i): step i works on buffer set i mod R."""
         nat, lib, w, J, N, B = self.nat, self.lib, self.w, self.J, self.N, self.rows
         p = lambda t: c_void_p(t.data_ptr())  # noqa: E731
         ctx = self.eng.ctx
         if self.pipeline == "fwd+inv":
             fwd = lib.vw_modwt_forward_f32 if self.f32 else lib.vw_modwt_forward_f64
             inv = lib.vw_modwt_inverse_f32 if self.f32 else lib.vw_modwt_inverse_f64
-            xp, dp, ap, yp = p(self.x), p(self.det), p(self.app), p(self.y)
+            ptrs = [(p(s["x"]), p(s["det"]), p(s["app"]), p(s["y"])) for s in self.sets]
 
-            def step():
+            def step(i=0):
+                r = i % self.rotate
+                self.last = r
+                xp, dp, ap, yp = ptrs[r]
                 self._check(fwd(ctx, xp, B, N, N, self.lo_a, self.hi_a, self.L, w.wavelet_id, nat.PERIODIC, J, flags,
                                 dp, ap))
                 self._check(inv(ctx, dp, ap, B, N, self.lo_a, self.hi_a, self.L, w.wavelet_id, nat.PERIODIC, J,
                                 0xFFFFFFFF, 0, flags, yp))
             return step
-        xp, yp, tp = p(self.x), p(self.y), p(self.thr)
+        ptrs = [(p(s["x"]), p(s["y"]), p(s["thr"])) for s in self.sets]
 
-        def step():
+        def step(i=0):
+            r = i % self.rotate
+            self.last = r
+            xp, yp, tp = ptrs[r]
             self._check(lib.vw_swt_denoise_f64(ctx, xp, B, N, N, self.lo_a, self.hi_a, self.L, w.wavelet_id,
                                                nat.PERIODIC, J, -1.0, 1, flags, yp, tp))
         return step
@@ -338,13 +378,15 @@ class Workload:
     row loads) -- the in-process form of DeviceGroup on one device (tools/concurrency_probe.py:
     4096 x 4096 db4 0.383 -> 0.369 ms per step at K = 2)."""
 
-    def __init__(self, engines, streams, w, J, rows, N, dtype, pipeline, row_offset, torch):
+    def __init__(self, engines, streams, w, J, rows, N, dtype, pipeline, row_offset, torch, rotate=1,
+                 rotate_outputs=False):
         from vectorwave_amd.shard import shard_rows
         K = min(len(engines), rows)
         self.parts = []
         for k in range(K):
             s0, r = shard_rows(rows, K, k)
-            self.parts.append(Part(engines[k], streams[k], w, J, r, N, dtype, pipeline, row_offset + s0, torch))
+            self.parts.append(Part(engines[k], streams[k], w, J, r, N, dtype, pipeline, row_offset + s0, torch,
+                                   rotate, rotate_outputs))
         self.rows, self.N, self.J, self.pipeline = rows, N, J, pipeline
         self.f32 = dtype == "f32"
         self.graphs = []
@@ -406,11 +448,24 @@ def measure(torch, dist, world, wl, flags, mode, steps, warmup, settle_s, events
         wl.graphs.extend(gs)
         return gs
 
+    R = max(pt.rotate for pt in parts)
+    ctr = [0]
+
+    def next_i():
+        ctr[0] += 1
+        return ctr[0] - 1
+
     if mode == "direct":
-        run1 = lambda: fork_join(lambda k: fns[k]())  # noqa: E731
+        def run1():
+            i = next_i()
+            fork_join(lambda k: fns[k](i))
     else:
-        g1 = capture_all(lambda k: fns[k])
-        run1 = lambda: fork_join(lambda k: g1[k].launch(1))  # noqa: E731
+        # one single-step graph per buffer set, cycled (settle / warmup / graph-step mode)
+        g1s = [capture_all(lambda k, r=r: (lambda: fns[k](r))) for r in range(R)]
+
+        def run1():
+            g = g1s[next_i() % R]
+            fork_join(lambda k: g[k].launch(1))
     # The timed body is prepared BEFORE the settle / warmup, so the timed replay follows the warmup with
     # no host-side capture gap in between (a GPU idle for milliseconds drops its clock again).
     sampled = 0
@@ -426,7 +481,7 @@ def measure(torch, dist, world, wl, flags, mode, steps, warmup, settle_s, events
             def record():
                 for i in range(steps):
                     eng.enable_timing(events and i % every == 0)
-                    fns[k]()
+                    fns[k](i)
                 eng.enable_timing(False)
             return record
         gk = capture_all(record_of)
@@ -548,7 +603,9 @@ def run(args, world, rank, local):
     K = args.contexts or (2 if rows >= 1024 else 1)
     engines = [vw.Engine.get(local)] + [vw.Engine(local) for _ in range(K - 1)]
     streams = [main] + [torch.cuda.Stream(device=dev) for _ in range(K - 1)]
-    wl = Workload(engines, streams, w, J, rows, N, dtype, pipeline, start, torch)
+    rot = (args.rotate, args.rotate_outputs)
+    wl = Workload(engines, streams, w, J, rows, N, dtype, pipeline, start, torch, *rot)
+    footprint = sum(pt.footprint() for pt in wl.parts)
     (elapsed, host_elapsed), (settle_s, settle_steps), fams, sampled, pass_ms = measure(
         torch, dist, world, wl, flags, args.launch, args.steps, args.warmup, args.settle, events)
     elapsed = max_over_ranks(torch, dist, world, elapsed, dev)
@@ -574,7 +631,7 @@ def run(args, world, rank, local):
     # graph method).  With K = 1 the headline's own launches are used.
     kfams, ksampled, kpass_ms = fams, sampled, pass_ms
     if K > 1 and events:
-        wk1 = Workload(engines[:1], streams[:1], w, J, rows, N, dtype, pipeline, start, torch)
+        wk1 = Workload(engines[:1], streams[:1], w, J, rows, N, dtype, pipeline, start, torch, *rot)
         _, _, kfams, ksampled, kpass_ms = measure(torch, dist, world, wk1, flags, args.launch, args.steps,
                                                   args.warmup, min(args.settle, 0.5), events)
         wk1.close()
@@ -640,7 +697,7 @@ def run(args, world, rank, local):
     # ---- weak scaling (N > 1): every rank owns a full per-GPU batch of Bg rows (the N = 1 workload)
     weak = None
     if world > 1 and not args.no_weak:
-        wk = Workload(engines, streams, w, J, Bg, N, dtype, pipeline, rank * Bg, torch)
+        wk = Workload(engines, streams, w, J, Bg, N, dtype, pipeline, rank * Bg, torch, *rot)
         (wel, _), _, _, _, _ = measure(torch, dist, world, wk, flags, args.launch, args.steps, args.warmup,
                                        min(args.settle, 0.3), False)
         wel = max_over_ranks(torch, dist, world, wel, dev)
@@ -682,6 +739,8 @@ def run(args, world, rank, local):
                                + (f", {K} contexts per GPU (own stream each, row blocks)" if K > 1 else ""),
                 "contexts_per_gpu": K,
                 "launch": LAUNCH_DESC[args.launch],
+                "buffer_sets": {"sets": args.rotate, "outputs_rotated": bool(args.rotate_outputs),
+                                "device_bytes_per_rank": footprint},
                 "passes_ms": {f: round(v, 5) for f, v in kpass_ms.items()},
                 "kernel_timing": (f"HIP events around every kernel launch of {sampled} of the {args.steps} timed "
                                   "steps (event nodes inside the replayed graph)" if args.launch == "graph-k" else

@@ -192,6 +192,26 @@ VW_API vw_status vw_modwt_inverse_multi_f64(vw_ctx *const *ctxs, int nctx, const
                                             const double *hi, int L, int wavelet_id, int boundary, int J,
                                             unsigned detail_mask, int approx_zero, unsigned flags, double *y);
 
+/* Device-resident form of the two calls above (each device has its own context,
+ * stream, input and output buffers; one host thread per device): context k works on ITS OWN device
+ * buffers -- x[k] is rows[k] x ldx on ctxs[k]'s device, details[k] is [J][rows[k]][N], approx[k] and
+ * y[k] are [rows[k]][N] -- so an FFM / JNI caller that keeps one batch shard resident per GPU calls all
+ * of them at once with no host staging.  Host thread k enqueues on ctxs[k]'s stream (ctxs[0] on the
+ * calling thread); the call returns when every context's work is enqueued, or finished with
+ * VW_FLAG_SYNC.  rows[k] = 0 skips context k.  VW_FLAG_HOST_MEMORY is refused (VW_ERR_ARG).  Errors:
+ * the first failing context's status; vw_last_error() names the context.
+ * Replaces: BatchMODWT.multiLevelAoS / inverseMultiLevelAoS (ext/extensions/modwt/BatchMODWT.java:90-111,
+ * :151-178) over a batch already sharded across devices. */
+VW_API vw_status vw_modwt_forward_multi_dev_f64(vw_ctx *const *ctxs, int nctx, const double *const *x,
+                                                const int64_t *rows, int64_t N, int64_t ldx, const double *lo,
+                                                const double *hi, int L, int wavelet_id, int boundary, int J,
+                                                unsigned flags, double *const *details, double *const *approx);
+VW_API vw_status vw_modwt_inverse_multi_dev_f64(vw_ctx *const *ctxs, int nctx, const double *const *details,
+                                                const double *const *approx, const int64_t *rows, int64_t N,
+                                                const double *lo, const double *hi, int L, int wavelet_id,
+                                                int boundary, int J, unsigned detail_mask, int approx_zero,
+                                                unsigned flags, double *const *y);
+
 /* ---- single-level MODWT (MODWTTransform: pairwise inverse sums, any N >= 1) --- */
 VW_API vw_status vw_modwt1_forward_f64(vw_ctx *ctx, const double *x, int64_t B, int64_t N, int64_t ldx,
                                        const double *lo, const double *hi, int L, int boundary,
@@ -247,8 +267,9 @@ VW_API vw_status vw_threshold_f64(vw_ctx *ctx, double *c, int64_t B, int64_t N, 
 /* core/modwt/streaming/MODWTStreamingDenoiser.java:133-272 with core/util/MathUtils.java:94-257.
  * median_out[b] = median(|x[b][:] - center[b]|) (center NULL: median(|x[b][:]|)), exact order
  * statistics, even N = mean of the middle pair (MathUtils.median); the two passes of
- * medianAbsoluteDeviation on non-negative data (any N; rows longer than 16384 with a center run the
- * deviations through the context workspace first). */
+ * medianAbsoluteDeviation on non-negative data (any N; rows longer than 16384 with a center write the
+ * deviations into a per-context scratch buffer first: it grows outside a capture only -- run such a
+ * call once before recording it -- and never moves the workspace that recorded graphs use). */
 VW_API vw_status vw_median_f64(vw_ctx *ctx, const double *x, int64_t B, int64_t N, const double *center,
                                unsigned flags, double *median_out);
 /* out[0] = MathUtils.standardDeviation(x[0..N)) -- sequential sums, sqrt(ssd / (N-1)); N >= 2. */

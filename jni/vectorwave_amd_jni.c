@@ -1,0 +1,296 @@
+/* vectorwave_amd_jni.c -- JNI glue between VectorWave's Java API and the MI355X engine's C-ABI
+ * (include/vectorwave_amd.h).  Built only where a JDK is present (jni/Makefile checks
+ * $JAVA_HOME/include/jni.h); the Java side is jni/java/com/morphiqlabs/wavelet/amd/AmdNative.java.
+ *
+ * One native call per batch, never one per row.  Two ways in:
+ *
+ *  - double[] arrays (the MODWTOptimizer SPI, core/api/spi/MODWTOptimizer.java:12-84, and the flat
+ *    batches of BatchMODWT.multiLevelAoS, ext/extensions/modwt/BatchMODWT.java:67-72): the arrays are
+ *    COPIED into native buffers (GetDoubleArrayRegion) and the results copied back
+ *    (SetDoubleArrayRegion).  No Java array is pinned while the GPU works, so the collector is never
+ *    blocked for the length of a transform (a critical section held across a multi-millisecond call
+ *    stalls every GC in the JVM).  The copies run at host memcpy speed, well above the PCIe staging
+ *    they precede.
+ *  - direct ByteBuffers (…Direct methods): the caller's off-heap memory goes straight to the engine's
+ *    host staging (GetDirectBufferAddress), no extra copy and no pinning; the FFM form of the same is
+ *    INTEGRATION.md §4.
+ *
+ * Every call passes VW_FLAG_HOST_MEMORY | VW_FLAG_SYNC: the engine stages through its per-context
+ * device pool and returns when the results are in the caller's memory.  Status codes are returned to
+ * Java unchanged; AmdNative.check() maps them to the reference's exceptions.
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "vectorwave_amd.h"
+
+#define VW_JNI(name) Java_com_morphiqlabs_wavelet_amd_AmdNative_##name
+#define HOST_FLAGS (VW_FLAG_HOST_MEMORY | VW_FLAG_SYNC)
+#define CTX(h) ((vw_ctx *)(intptr_t)(h))
+
+/* Per-thread native copy buffers, reused across calls (a JVM worker transforms batch after batch).
+ * Slot 0..3: inputs / outputs of one call.  Buffers above kKeepBytes are released after the call. */
+enum { kSlots = 4 };
+static const size_t kKeepBytes = (size_t)256 << 20;
+static __thread double *t_buf[kSlots];
+static __thread size_t t_cap[kSlots];
+
+static double *slot(int k, size_t count) {
+  size_t bytes = (count ? count : 1) * sizeof(double);
+  if (bytes > t_cap[k]) {
+    free(t_buf[k]);
+    t_buf[k] = (double *)malloc(bytes);
+    t_cap[k] = t_buf[k] ? bytes : 0;
+  }
+  return t_buf[k];
+}
+
+static void trim_slots(void) {
+  for (int k = 0; k < kSlots; ++k)
+    if (t_cap[k] > kKeepBytes) {
+      free(t_buf[k]);
+      t_buf[k] = NULL;
+      t_cap[k] = 0;
+    }
+}
+
+/* Copy a Java double[] (count elements) into native slot k; NULL array -> NULL. */
+static double *copy_in(JNIEnv *e, jdoubleArray a, int k, size_t count, int *oom) {
+  if (!a) return NULL;
+  double *p = slot(k, count);
+  if (!p) { *oom = 1; return NULL; }
+  if (count) (*e)->GetDoubleArrayRegion(e, a, 0, (jsize)count, p);
+  return p;
+}
+
+static double *out_buf(int k, size_t count, int *oom) {
+  double *p = slot(k, count);
+  if (!p) *oom = 1;
+  return p;
+}
+
+static void copy_out(JNIEnv *e, jdoubleArray a, const double *p, size_t count) {
+  if (a && p && count) (*e)->SetDoubleArrayRegion(e, a, 0, (jsize)count, p);
+}
+
+/* Taps are short (<= 64): a stack copy. */
+typedef struct { double v[64]; int n; } Taps;
+static int get_taps(JNIEnv *e, jdoubleArray a, Taps *t) {
+  if (!a) return 0;
+  t->n = (*e)->GetArrayLength(e, a);
+  if (t->n < 1 || t->n > 64) return 0;
+  (*e)->GetDoubleArrayRegion(e, a, 0, t->n, t->v);
+  return 1;
+}
+
+static size_t alen(JNIEnv *e, jdoubleArray a) { return a ? (size_t)(*e)->GetArrayLength(e, a) : 0; }
+
+/* ---- contexts ------------------------------------------------------------------------------ */
+JNIEXPORT jlong JNICALL VW_JNI(ctxCreate)(JNIEnv *e, jclass c, jint device) {
+  (void)e; (void)c;
+  vw_ctx *ctx = NULL;
+  return vw_ctx_create(device, &ctx) == VW_OK ? (jlong)(intptr_t)ctx : 0;
+}
+
+JNIEXPORT jint JNICALL VW_JNI(ctxDestroy)(JNIEnv *e, jclass c, jlong ctx) {
+  (void)e; (void)c;
+  return vw_ctx_destroy(CTX(ctx));
+}
+
+JNIEXPORT jint JNICALL VW_JNI(maxLevels)(JNIEnv *e, jclass c, jlong n, jint L) {
+  (void)e; (void)c;
+  return vw_max_levels(n, L);
+}
+
+JNIEXPORT jstring JNICALL VW_JNI(lastError)(JNIEnv *e, jclass c) {
+  (void)c;
+  return (*e)->NewStringUTF(e, vw_last_error());
+}
+
+JNIEXPORT jlong JNICALL VW_JNI(lastErrorIndex)(JNIEnv *e, jclass c) {
+  (void)e; (void)c;
+  return vw_last_error_index();
+}
+
+/* ---- single level: MODWTTransform.forward / forwardBatch, inverse / inverseBatch ------------- */
+/* x: B*N (row-major), approx / detail: B*N.  MODWTOptimizer.forward is B = 1. */
+JNIEXPORT jint JNICALL VW_JNI(modwt1Forward)(JNIEnv *e, jclass c, jlong ctx, jdoubleArray x, jint B, jint N,
+                                             jdoubleArray lo, jdoubleArray hi, jint boundary, jint flags,
+                                             jdoubleArray approx, jdoubleArray detail) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n) return VW_ERR_ARG;
+  const size_t n = (size_t)B * (size_t)N;
+  if (alen(e, x) < n || alen(e, approx) < n || alen(e, detail) < n) return VW_ERR_ARG;
+  int oom = 0;
+  double *px = copy_in(e, x, 0, n, &oom), *pa = out_buf(1, n, &oom), *pd = out_buf(2, n, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = vw_modwt1_forward_f64(CTX(ctx), px, B, N, N, tl.v, th.v, tl.n, boundary,
+                                       (unsigned)flags | HOST_FLAGS, pa, pd);
+  if (st == VW_OK) { copy_out(e, approx, pa, n); copy_out(e, detail, pd, n); }
+  trim_slots();
+  return st;
+}
+
+JNIEXPORT jint JNICALL VW_JNI(modwt1Inverse)(JNIEnv *e, jclass c, jlong ctx, jdoubleArray approx,
+                                             jdoubleArray detail, jint B, jint N, jdoubleArray lo, jdoubleArray hi,
+                                             jint boundary, jint flags, jdoubleArray y) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n) return VW_ERR_ARG;
+  const size_t n = (size_t)B * (size_t)N;
+  if (alen(e, approx) < n || alen(e, detail) < n || alen(e, y) < n) return VW_ERR_ARG;
+  int oom = 0;
+  double *pa = copy_in(e, approx, 0, n, &oom), *pd = copy_in(e, detail, 1, n, &oom), *py = out_buf(2, n, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = vw_modwt1_inverse_f64(CTX(ctx), pa, pd, B, N, tl.v, th.v, tl.n, boundary,
+                                       (unsigned)flags | HOST_FLAGS, py);
+  if (st == VW_OK) copy_out(e, y, py, n);
+  trim_slots();
+  return st;
+}
+
+/* ---- multi level: MultiLevelMODWTTransform.decompose / reconstruct, BatchMODWT.multiLevelAoS -- */
+/* x: B*N, details: J*B*N ([level 1..J][B][N]), approx: B*N. */
+JNIEXPORT jint JNICALL VW_JNI(modwtForward)(JNIEnv *e, jclass c, jlong ctx, jdoubleArray x, jint B, jint N,
+                                            jdoubleArray lo, jdoubleArray hi, jint wid, jint boundary, jint J,
+                                            jint flags, jdoubleArray details, jdoubleArray approx) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n || J < 1) return VW_ERR_ARG;
+  const size_t n = (size_t)B * (size_t)N;
+  if (alen(e, x) < n || alen(e, details) < (size_t)J * n || alen(e, approx) < n) return VW_ERR_ARG;
+  int oom = 0;
+  double *px = copy_in(e, x, 0, n, &oom), *pd = out_buf(1, (size_t)J * n, &oom), *pa = out_buf(2, n, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = vw_modwt_forward_f64(CTX(ctx), px, B, N, N, tl.v, th.v, tl.n, wid, boundary, J,
+                                      (unsigned)flags | HOST_FLAGS, pd, pa);
+  if (st == VW_OK) { copy_out(e, details, pd, (size_t)J * n); copy_out(e, approx, pa, n); }
+  trim_slots();
+  return st;
+}
+
+JNIEXPORT jint JNICALL VW_JNI(modwtInverse)(JNIEnv *e, jclass c, jlong ctx, jdoubleArray details,
+                                            jdoubleArray approx, jint B, jint N, jdoubleArray lo, jdoubleArray hi,
+                                            jint wid, jint boundary, jint J, jint detailMask, jboolean approxZero,
+                                            jint flags, jdoubleArray y) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n || J < 1) return VW_ERR_ARG;
+  const size_t n = (size_t)B * (size_t)N;
+  if ((detailMask && alen(e, details) < (size_t)J * n) || (!approxZero && alen(e, approx) < n) || alen(e, y) < n)
+    return VW_ERR_ARG;
+  int oom = 0;
+  double *pd = detailMask ? copy_in(e, details, 0, (size_t)J * n, &oom) : NULL;
+  double *pa = approxZero ? NULL : copy_in(e, approx, 1, n, &oom);
+  double *py = out_buf(2, n, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = vw_modwt_inverse_f64(CTX(ctx), pd, pa, B, N, tl.v, th.v, tl.n, wid, boundary, J,
+                                      (unsigned)detailMask, approxZero ? 1 : 0, (unsigned)flags | HOST_FLAGS, py);
+  if (st == VW_OK) copy_out(e, y, py, n);
+  trim_slots();
+  return st;
+}
+
+/* One batch over several contexts (one std::thread per context inside the engine). */
+JNIEXPORT jint JNICALL VW_JNI(modwtForwardMulti)(JNIEnv *e, jclass c, jlongArray ctxs, jdoubleArray x, jint B,
+                                                 jint N, jdoubleArray lo, jdoubleArray hi, jint wid, jint boundary,
+                                                 jint J, jint flags, jdoubleArray details, jdoubleArray approx) {
+  (void)c;
+  Taps tl, th;
+  if (!ctxs || !get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n || J < 1) return VW_ERR_ARG;
+  const jsize nctx = (*e)->GetArrayLength(e, ctxs);
+  if (nctx < 1 || nctx > 256) return VW_ERR_ARG;
+  jlong hs[256];
+  (*e)->GetLongArrayRegion(e, ctxs, 0, nctx, hs);
+  vw_ctx *cs[256];
+  for (jsize k = 0; k < nctx; ++k) cs[k] = CTX(hs[k]);
+  const size_t n = (size_t)B * (size_t)N;
+  if (alen(e, x) < n || alen(e, details) < (size_t)J * n || alen(e, approx) < n) return VW_ERR_ARG;
+  int oom = 0;
+  double *px = copy_in(e, x, 0, n, &oom), *pd = out_buf(1, (size_t)J * n, &oom), *pa = out_buf(2, n, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = vw_modwt_forward_multi_f64(cs, nctx, px, B, N, N, tl.v, th.v, tl.n, wid, boundary, J,
+                                            (unsigned)flags | VW_FLAG_HOST_MEMORY, pd, pa);
+  if (st == VW_OK) { copy_out(e, details, pd, (size_t)J * n); copy_out(e, approx, pa, n); }
+  trim_slots();
+  return st;
+}
+
+/* ---- denoising: VectorWaveSwtAdapter.denoise, WaveletDenoiser ------------------------------ */
+JNIEXPORT jint JNICALL VW_JNI(swtDenoise)(JNIEnv *e, jclass c, jlong ctx, jdoubleArray x, jint B, jint N,
+                                          jdoubleArray lo, jdoubleArray hi, jint wid, jint boundary, jint J,
+                                          jdouble threshold, jboolean soft, jint flags, jdoubleArray y,
+                                          jdoubleArray thresholdsOut) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n) return VW_ERR_ARG;
+  const size_t n = (size_t)B * (size_t)N;
+  if (alen(e, x) < n || alen(e, y) < n || (thresholdsOut && alen(e, thresholdsOut) < (size_t)B)) return VW_ERR_ARG;
+  int oom = 0;
+  double *px = copy_in(e, x, 0, n, &oom), *py = out_buf(1, n, &oom);
+  double *pt = thresholdsOut ? out_buf(2, (size_t)B, &oom) : NULL;
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = vw_swt_denoise_f64(CTX(ctx), px, B, N, N, tl.v, th.v, tl.n, wid, boundary, J, threshold,
+                                    soft ? 1 : 0, (unsigned)flags | HOST_FLAGS, py, pt);
+  if (st == VW_OK) { copy_out(e, y, py, n); copy_out(e, thresholdsOut, pt, (size_t)B); }
+  trim_slots();
+  return st;
+}
+
+JNIEXPORT jint JNICALL VW_JNI(waveletDenoise)(JNIEnv *e, jclass c, jlong ctx, jdoubleArray x, jint B, jint N,
+                                              jdoubleArray lo, jdoubleArray hi, jint wid, jint boundary,
+                                              jint levels, jint method, jdouble fixedThreshold, jboolean soft,
+                                              jint flags, jdoubleArray y, jdoubleArray thresholdsOut) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n) return VW_ERR_ARG;
+  const size_t n = (size_t)B * (size_t)N, nt = (size_t)(levels > 0 ? levels : 1) * (size_t)B;
+  if (alen(e, x) < n || alen(e, y) < n || (thresholdsOut && alen(e, thresholdsOut) < nt)) return VW_ERR_ARG;
+  int oom = 0;
+  double *px = copy_in(e, x, 0, n, &oom), *py = out_buf(1, n, &oom);
+  double *pt = thresholdsOut ? out_buf(2, nt, &oom) : NULL;
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = vw_wavelet_denoise_f64(CTX(ctx), px, B, N, N, tl.v, th.v, tl.n, wid, boundary, levels, method,
+                                        fixedThreshold, soft ? 1 : 0, (unsigned)flags | HOST_FLAGS, py, pt);
+  if (st == VW_OK) { copy_out(e, y, py, n); copy_out(e, thresholdsOut, pt, nt); }
+  trim_slots();
+  return st;
+}
+
+/* ---- direct ByteBuffers: zero-copy host path ----------------------------------------------- */
+static double *direct(JNIEnv *e, jobject buf, size_t count) {
+  if (!buf) return NULL;
+  void *p = (*e)->GetDirectBufferAddress(e, buf);
+  jlong cap = (*e)->GetDirectBufferCapacity(e, buf);
+  if (!p || cap < 0 || (size_t)cap < count * sizeof(double)) return NULL;
+  return (double *)p;
+}
+
+JNIEXPORT jint JNICALL VW_JNI(modwtForwardDirect)(JNIEnv *e, jclass c, jlong ctx, jobject x, jint B, jint N,
+                                                  jdoubleArray lo, jdoubleArray hi, jint wid, jint boundary, jint J,
+                                                  jint flags, jobject details, jobject approx) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n || J < 1) return VW_ERR_ARG;
+  const size_t n = (size_t)B * (size_t)N;
+  double *px = direct(e, x, n), *pd = direct(e, details, (size_t)J * n), *pa = direct(e, approx, n);
+  if (!px || !pd || !pa) return VW_ERR_ARG;  /* not direct, or too small */
+  return vw_modwt_forward_f64(CTX(ctx), px, B, N, N, tl.v, th.v, tl.n, wid, boundary, J,
+                              (unsigned)flags | HOST_FLAGS, pd, pa);
+}
+
+JNIEXPORT jint JNICALL VW_JNI(modwtInverseDirect)(JNIEnv *e, jclass c, jlong ctx, jobject details, jobject approx,
+                                                  jint B, jint N, jdoubleArray lo, jdoubleArray hi, jint wid,
+                                                  jint boundary, jint J, jint flags, jobject y) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n || J < 1) return VW_ERR_ARG;
+  const size_t n = (size_t)B * (size_t)N;
+  double *pd = direct(e, details, (size_t)J * n), *pa = direct(e, approx, n), *py = direct(e, y, n);
+  if (!pd || !pa || !py) return VW_ERR_ARG;
+  return vw_modwt_inverse_f64(CTX(ctx), pd, pa, B, N, tl.v, th.v, tl.n, wid, boundary, J, 0xFFFFFFFFu, 0,
+                              (unsigned)flags | HOST_FLAGS, py);
+}

@@ -111,11 +111,13 @@ def test_no_collective_inside_timed_interval():
             return []
 
     class Part:
+        rotate = 2   # two buffer sets: the timed steps alternate, still one replay per context
+
         def __init__(self):
             self.eng, self.stream = Eng(), Stream()
 
         def step_fn(self, flags):
-            return lambda: log.append("step")
+            return lambda i=0: log.append("step")
 
     class Wl:
         def __init__(self):

@@ -70,6 +70,17 @@ def test_capture_refuses_synchronizing_calls(engine):
         st = lib.vw_modwt_forward_f64(ctx, c_void_p(x.data_ptr()), 4, 512, 512, lo, hi, len(lo), w.wavelet_id, 0, 3,
                                       nat.FLAG_VALIDATE, c_void_p(det.data_ptr()), c_void_p(app.data_ptr()))
         assert st == 10  # VW_ERR_STATE
+        # a host-memory (JNI-shaped) call is refused before it stages anything: the capture
+        # stays valid and ends cleanly
+        xh, dh, ah = np.zeros((4, 512)), np.empty((3, 4, 512)), np.empty((4, 512))
+        for fn, args in ((lib.vw_modwt_forward_f64, (c_void_p(xh.ctypes.data), 4, 512, 512, lo, hi, len(lo),
+                                                     w.wavelet_id, 0, 3, nat.FLAG_HOST_MEMORY,
+                                                     c_void_p(dh.ctypes.data), c_void_p(ah.ctypes.data))),
+                         (lib.vw_modwt_inverse_f64, (c_void_p(dh.ctypes.data), c_void_p(ah.ctypes.data), 4, 512,
+                                                     lo, hi, len(lo), w.wavelet_id, 0, 3, 0xFFFFFFFF, 0,
+                                                     nat.FLAG_HOST_MEMORY, c_void_p(xh.ctypes.data)))):
+            assert fn(ctx, *args) == 10
+            assert "captured" in nat.last_error()
         assert lib.vw_capture_begin(ctx) == 10  # already capturing
         g = c_void_p()
         assert lib.vw_capture_end(ctx, byref(g)) == 0

@@ -63,7 +63,9 @@ def test_sharded_errors_name_the_block(engine):
                                                   O.PERIODIC, 2, nat.FLAG_HOST_MEMORY | nat.FLAG_VALIDATE,
                                                   det.ctypes.data_as(c_void_p), app.ctypes.data_as(c_void_p)))
         assert ei.value.index == 17
-        assert "block 1" in nat.last_error()
+        msg = nat.last_error()
+        # the block, its global rows, and the signal counted from row 0 of the whole batch
+        assert "block 1 (rows 2..3)" in msg and "(signal 3)" in msg, msg
         # device memory is refused (each block must be staged through its own context)
         st = lib.vw_modwt_forward_multi_f64(g._ctxs, 2, x.ctypes.data_as(c_void_p), 4, 256, 256,
                                             nat.taps_array(w.lowPassDecomposition()),
@@ -110,21 +112,46 @@ def test_four_threads_hammer_one_context(engine):
 
 
 def test_device_tensors_one_thread_per_context(engine):
+    """vw_modwt_forward/inverse_multi_dev_f64: each context works on its own device
+    buffers (uneven shards, an empty one), no staging; bit-exact vs the restatement in EXACT mode and
+    within 1e-12 with FMA; the inverse round trip too."""
     import torch
     w = Daubechies.DB4
     n, J = 4096, 6
-    with vw.DeviceGroup([0, 0]) as g:
-        xs = []
-        for k in range(2):
-            x = torch.empty((64, n), dtype=torch.float64, device="cuda")
-            engine.fill_uniform(x, 42, offset=k * 64 * n)
+    rows = [64, 37, 0]
+    with vw.DeviceGroup([0, 0, 0]) as g:
+        xs, off = [], 0
+        for r in rows:
+            x = torch.empty((r, n), dtype=torch.float64, device="cuda")
+            if r:
+                engine.fill_uniform(x, 42, offset=off * n)
+            off += r
             xs.append(x)
         torch.cuda.synchronize()
-        outs = g.forward_device(xs, w, J)
-        torch.cuda.synchronize()
-        for k, (d, a) in enumerate(outs):
-            for b in (0, 63):
-                d_ref, a_ref = O.decompose(xs[k][b].cpu().numpy(), w.lowPassDecomposition(),
-                                           w.highPassDecomposition(), O.PERIODIC, J, core=False)
-                assert np.array_equal(d[:, b].cpu().numpy(), d_ref)
-                assert np.array_equal(a[b].cpu().numpy(), a_ref)
+        for fma in (False, True):
+            outs = g.forward_device(xs, w, J, fma=fma)
+            ys = g.inverse_device(outs, w, fma=fma)
+            for k, ((d, a), y) in enumerate(zip(outs, ys)):
+                assert d.shape == (J, rows[k], n) and y.shape == (rows[k], n)
+                for b in ({0, rows[k] - 1} if rows[k] else ()):
+                    xr = xs[k][b].cpu().numpy()
+                    d_ref, a_ref = O.decompose(xr, w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC,
+                                               J, core=False)
+                    y_ref = O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(),
+                                          O.PERIODIC)
+                    if fma:
+                        assert np.abs(d[:, b].cpu().numpy() - d_ref).max() <= 1e-12
+                        assert np.abs(y[b].cpu().numpy() - y_ref).max() <= 1e-12
+                    else:
+                        assert np.array_equal(d[:, b].cpu().numpy(), d_ref)
+                        assert np.array_equal(a[b].cpu().numpy(), a_ref)
+                        assert np.array_equal(y[b].cpu().numpy(), y_ref)
+        # the device path refuses the host flag, and the host path still refuses device memory
+        lib = nat.load()
+        from ctypes import c_int64, c_void_p
+        ptrs = (c_void_p * 3)(*[x.data_ptr() for x in xs])
+        rr = (c_int64 * 3)(*rows)
+        st = lib.vw_modwt_forward_multi_dev_f64(g._ctxs, 3, ptrs, rr, n, n, nat.taps_array(w.lowPassDecomposition()),
+                                                nat.taps_array(w.highPassDecomposition()), 8, w.wavelet_id,
+                                                O.PERIODIC, J, nat.FLAG_HOST_MEMORY, ptrs, ptrs)
+        assert st == 7   # VW_ERR_ARG

@@ -55,6 +55,11 @@ SIGNATURES = {
                                            c_int, c_int, c_int, c_uint, c_void_p, c_void_p]),
     "vw_modwt_inverse_multi_f64": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int64, _dp, _dp, c_int,
                                            c_int, c_int, c_int, c_uint, c_int, c_uint, c_void_p]),
+    # device-resident: per-context arrays of device pointers (c_void_p * n) and rows (c_int64 * n)
+    "vw_modwt_forward_multi_dev_f64": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_int64, c_int64, _dp, _dp,
+                                               c_int, c_int, c_int, c_int, c_uint, c_void_p, c_void_p]),
+    "vw_modwt_inverse_multi_dev_f64": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int64, _dp, _dp,
+                                               c_int, c_int, c_int, c_int, c_uint, c_int, c_uint, c_void_p]),
     "vw_modwt1_forward_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, _dp, _dp, c_int, c_int, c_uint,
                                       c_void_p, c_void_p]),
     "vw_modwt1_inverse_f64": (c_int, [c_void_p, c_void_p, c_void_p, c_int64, c_int64, _dp, _dp, c_int, c_int, c_uint,

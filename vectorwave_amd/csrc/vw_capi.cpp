@@ -25,6 +25,7 @@ using namespace vw;
 // Errors (thread-local, like the reference's exceptions are per call site)
 static thread_local std::string t_err;
 static thread_local int64_t t_err_index = -1;
+static thread_local int64_t t_signal_base = 0;  // run_sharded: global row of this block's first signal
 
 static vw_status fail(vw_status code, const char* fmt, ...) {
   char buf[512];
@@ -188,6 +189,8 @@ struct vw_ctx {
   std::map<std::string, std::pair<double, int64_t>> totals;
   std::set<vw_graph*> graphs;          // live graphs recorded on this context (invalidated at destroy)
   std::vector<std::pair<void*, size_t>> stage;  // host-memory staging pool (Staging), kept across calls
+  void* med = nullptr;         // vw_median_f64 deviations of long rows (not ws: growing ws invalidates graphs)
+  size_t med_bytes = 0;
 };
 
 struct vw_graph {
@@ -471,6 +474,7 @@ extern "C" vw_status vw_ctx_destroy(vw_ctx* c) {
   for (auto e : c->event_pool) hipEventDestroy(e);
   if (c->ws) hipFree(c->ws);
   if (c->ws2) hipFree(c->ws2);
+  if (c->med) hipFree(c->med);
   for (auto& b : c->stage) hipFree(b.first);
   if (c->bad) hipFree(c->bad);
   if (c->own_stream) hipStreamDestroy(c->stream);
@@ -751,7 +755,7 @@ static vw_status report_bad(unsigned long long bad, int64_t N) {
   t_err_index = (int64_t)(flat % (unsigned long long)N);
   return fail(VW_ERR_NONFINITE, "%s contains non-finite value at index %lld (signal %lld)",
               out ? "coefficients" : "signal", (long long)(flat % (unsigned long long)N),
-              (long long)(flat / (unsigned long long)N));
+              (long long)(flat / (unsigned long long)N) + (long long)t_signal_base);
 }
 
 // Plan of a fused launch: threads, vectors per thread (4 or 8), LDS bytes.  NV = 4 keeps the
@@ -1479,7 +1483,22 @@ struct Staging {
   vw_ctx* c;
   size_t used_block = 0, used_off = 0;
   explicit Staging(vw_ctx* ctx) : c(ctx) {}
-  ~Staging() { hipStreamSynchronize(c->stream); }
+  // After the call's copies and kernels: keep only the largest block (the next call of the same
+  // shape allocates at most one block >= its whole need, and frees this one here), so the pool holds
+  // one block of about the largest call's size instead of every block it ever grew through.
+  ~Staging() {
+    hipStreamSynchronize(c->stream);
+    if (c->stage.size() > 1) {
+      auto big = std::max_element(c->stage.begin(), c->stage.end(),
+                                  [](const std::pair<void*, size_t>& a, const std::pair<void*, size_t>& b) {
+                                    return a.second < b.second;
+                                  });
+      const auto keep = *big;
+      for (auto& blk : c->stage)
+        if (blk.first != keep.first) hipFree(blk.first);
+      c->stage.assign(1, keep);
+    }
+  }
   vw_status carve(size_t bytes, void** out) {
     bytes = align_up(std::max<size_t>(bytes, 16), 256);
     for (; used_block < c->stage.size(); ++used_block, used_off = 0) {
@@ -1490,8 +1509,12 @@ struct Staging {
         return VW_OK;
       }
     }
-    const size_t last = c->stage.empty() ? 0 : c->stage.back().second;
-    const size_t want = std::max({bytes, 2 * last, (size_t)4 << 20});
+    // a new block covers everything this call has carved so far plus this request, so the pool
+    // converges to one block per call shape (see the destructor)
+    size_t carved = bytes;
+    for (size_t k = 0; k < used_block && k < c->stage.size(); ++k) carved += c->stage[k].second;
+    if (used_block < c->stage.size()) carved += used_off;
+    const size_t want = std::max({carved, (size_t)4 << 20});
     void* p = nullptr;
     VW_HIP(hipMalloc(&p, want));
     c->stage.push_back({p, want});
@@ -1542,6 +1565,7 @@ template <typename T>
 static vw_status forward_host(vw_ctx* c, const T* x, int64_t B, int64_t N, int64_t ldx, const double* lo,
                               const double* hi, int L, int boundary, int J, unsigned flags, T* details,
                               int64_t det_stride, T* approx) {
+  if (c->capturing) return fail(VW_ERR_STATE, "host-memory calls cannot be captured (they synchronize)");
   Staging s(c);
   T *dx, *dd, *da;
   VW_TRY(s.in(x, (size_t)(B - 1) * ldx + N, &dx));  // (the last row's padding need not exist)
@@ -1559,6 +1583,7 @@ template <typename T>
 static vw_status inverse_host(vw_ctx* c, const T* details, int64_t det_stride, const T* approx, int64_t B, int64_t N,
                               const double* lo, const double* hi, int L, int wid, int boundary, int J,
                               unsigned detail_mask, int approx_zero, unsigned flags, T* y) {
+  if (c->capturing) return fail(VW_ERR_STATE, "host-memory calls cannot be captured (they synchronize)");
   Staging s(c);
   T *dd = nullptr, *da = nullptr, *dy;
   if (detail_mask) VW_TRY(s.in_planes(details, (size_t)J, (size_t)(B * N), (size_t)det_stride, &dd));
@@ -1653,6 +1678,35 @@ static void shard_block(int64_t B, int n, int k, int64_t* start, int64_t* rows) 
   *rows = base + (k < extra ? 1 : 0);
 }
 
+// fn(k) on context k, one host thread per context (k = 0 on the calling thread); the first failing
+// context's status, its message prefixed with `what` k.
+template <typename F>
+static vw_status run_per_ctx(vw_ctx* const* ctxs, int nctx, const char* what, F&& fn) {
+  if (!ctxs) return fail(VW_ERR_NULL, "ctxs is null");
+  if (nctx < 1) return fail(VW_ERR_ARG, "need at least one context (got %d)", nctx);
+  for (int k = 0; k < nctx; ++k)
+    if (!ctxs[k]) return fail(VW_ERR_NULL, "ctxs[%d] is null", k);
+  struct Res { vw_status st = VW_OK; std::string msg; int64_t idx = -1; };
+  std::vector<Res> res(nctx);
+  auto work = [&](int k) {
+    const vw_status st = fn(k);
+    res[k].st = st;
+    if (st != VW_OK) { res[k].msg = t_err; res[k].idx = t_err_index; }
+  };
+  std::vector<std::thread> th;
+  th.reserve(nctx);
+  for (int k = 1; k < nctx; ++k) th.emplace_back(work, k);
+  work(0);
+  for (auto& t : th) t.join();
+  for (int k = 0; k < nctx; ++k)
+    if (res[k].st != VW_OK) {
+      t_err = std::string(what) + " " + std::to_string(k) + ": " + res[k].msg;
+      t_err_index = res[k].idx;
+      return res[k].st;
+    }
+  return ok();
+}
+
 template <typename F>
 static vw_status run_sharded(vw_ctx* const* ctxs, int nctx, int64_t B, F&& fn) {
   if (!ctxs) return fail(VW_ERR_NULL, "ctxs is null");
@@ -1666,7 +1720,9 @@ static vw_status run_sharded(vw_ctx* const* ctxs, int nctx, int64_t B, F&& fn) {
   auto work = [&](int k) {
     int64_t start, rows;
     shard_block(B, used, k, &start, &rows);
+    t_signal_base = start;  // signal numbers in this thread's error messages count from row 0 of the batch
     const vw_status st = fn(ctxs[k], start, rows);
+    t_signal_base = 0;
     res[k].st = st;
     if (st != VW_OK) { res[k].msg = t_err; res[k].idx = t_err_index; }
   };
@@ -1677,7 +1733,10 @@ static vw_status run_sharded(vw_ctx* const* ctxs, int nctx, int64_t B, F&& fn) {
   for (auto& t : th) t.join();
   for (int k = 0; k < used; ++k)
     if (res[k].st != VW_OK) {
-      t_err = "block " + std::to_string(k) + ": " + res[k].msg;
+      int64_t start, rows;
+      shard_block(B, used, k, &start, &rows);
+      t_err = "block " + std::to_string(k) + " (rows " + std::to_string(start) + ".." +
+              std::to_string(start + rows - 1) + "): " + res[k].msg;
       t_err_index = res[k].idx;
       return res[k].st;
     }
@@ -1720,6 +1779,37 @@ extern "C" vw_status vw_modwt_inverse_multi_f64(vw_ctx* const* ctxs, int nctx, c
     return inverse_host<double>(c, details ? details + start * N : nullptr, B * N,
                                 approx ? approx + start * N : nullptr, rows, N, lo, hi, L, wid, boundary, J,
                                 detail_mask, approx_zero, flags, y + start * N);
+  });
+}
+
+extern "C" vw_status vw_modwt_forward_multi_dev_f64(vw_ctx* const* ctxs, int nctx, const double* const* x,
+                                                    const int64_t* rows, int64_t N, int64_t ldx, const double* lo,
+                                                    const double* hi, int L, int wid, int boundary, int J,
+                                                    unsigned flags, double* const* details,
+                                                    double* const* approx) {
+  if (flags & VW_FLAG_HOST_MEMORY)
+    return fail(VW_ERR_ARG, "device-resident multi-context calls take device memory (no VW_FLAG_HOST_MEMORY)");
+  if (!x || !rows || !details || !approx) return fail(VW_ERR_NULL, "null array argument");
+  return run_per_ctx(ctxs, nctx, "context", [&](int k) -> vw_status {
+    if (rows[k] == 0) return VW_OK;
+    return modwt_forward<double>(ctxs[k], x[k], rows[k], N, ldx, lo, hi, L, wid, boundary, J, flags, details[k],
+                                 approx[k]);
+  });
+}
+
+extern "C" vw_status vw_modwt_inverse_multi_dev_f64(vw_ctx* const* ctxs, int nctx, const double* const* details,
+                                                    const double* const* approx, const int64_t* rows, int64_t N,
+                                                    const double* lo, const double* hi, int L, int wid,
+                                                    int boundary, int J, unsigned detail_mask, int approx_zero,
+                                                    unsigned flags, double* const* y) {
+  if (flags & VW_FLAG_HOST_MEMORY)
+    return fail(VW_ERR_ARG, "device-resident multi-context calls take device memory (no VW_FLAG_HOST_MEMORY)");
+  if (!rows || !y || (!details && detail_mask) || (!approx && !approx_zero))
+    return fail(VW_ERR_NULL, "null array argument");
+  return run_per_ctx(ctxs, nctx, "context", [&](int k) -> vw_status {
+    if (rows[k] == 0) return VW_OK;
+    return modwt_inverse<double>(ctxs[k], details ? details[k] : nullptr, approx ? approx[k] : nullptr, rows[k], N,
+                                 lo, hi, L, wid, boundary, J, detail_mask, approx_zero, flags, y[k]);
   });
 }
 
@@ -2080,8 +2170,20 @@ extern "C" vw_status vw_median_f64(vw_ctx* c, const double* x, int64_t B, int64_
     // rows beyond the register-keyed centered path: deviations |x - center| into the workspace, then
     // the uncentered selection (any N) on them -- the same keys, the same exact order statistic
     if (B > 65535) return fail(VW_ERR_UNSUPPORTED, "centered median of more than 65535 long rows");
-    VW_TRY(ensure_ws(c, (size_t)B * (size_t)N * sizeof(double)));
-    double* dev = reinterpret_cast<double*>(c->ws);
+    const size_t need = (size_t)B * (size_t)N * sizeof(double);
+    if (need > c->med_bytes) {
+      if (c->capturing)
+        return fail(VW_ERR_STATE, "median scratch growth during capture: run the call once before capturing it");
+      if (c->med) {
+        VW_HIP(hipStreamSynchronize(c->stream));  // only this context's stream ever uses the scratch
+        hipFree(c->med);
+        c->med = nullptr;
+        c->med_bytes = 0;
+      }
+      VW_HIP(hipMalloc(&c->med, need));
+      c->med_bytes = need;
+    }
+    double* dev = reinterpret_cast<double*>(c->med);
     e = launch_abs_center(x, N, B, (int)N, center, dev, c->stream);
     if (e == hipSuccess) e = launch_median(dev, N, B, (int)N, nullptr, median_out, c->stream);
   } else {

@@ -417,7 +417,7 @@ __global__ void __launch_bounds__(kDeepThreads) k_inverse_deep(const DeepArgs<T>
 template <typename T, int L, bool FMA, bool INV>
 static hipError_t run_deep(const DeepArgs<T>& a, int lds, hipStream_t st) {
   auto k = INV ? k_inverse_deep<T, L, FMA> : k_forward_deep<T, L, FMA>;
-  static int configured = 64 * 1024;
+  static LdsOnce configured;
   hipError_t e = set_lds(k, lds, &configured);
   if (e != hipSuccess) return e;
   const long long groups = (a.B * a.seg + 7) / 8 * 8;

@@ -8,7 +8,7 @@ template <typename T, int L, bool FMA, int NV>
 static hipError_t run_forward_fused_nv(const FwdArgs<T>& a, int threads, int lds, hipStream_t st) {
   const bool hist = a.hist[0] != nullptr;
   auto k = hist ? k_forward_fused<T, L, FMA, NV, true> : k_forward_fused<T, L, FMA, NV, false>;
-  static int configured = 64 * 1024, configured_h = 64 * 1024;
+  static LdsOnce configured, configured_h;
   hipError_t e = set_lds(k, lds, hist ? &configured_h : &configured);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(threads), lds, st, a);
@@ -39,7 +39,7 @@ template hipError_t launch_forward_fused<VW_T>(const FwdArgs<VW_T>&, int, int, b
 template <typename T, int L, bool FMA, int NV>
 static hipError_t run_forward_blk_nv(const FwdArgs<T>& a, int threads, int lds, hipStream_t st) {
   auto k = k_forward_blk<T, L, FMA, NV>;
-  static int configured = 64 * 1024;
+  static LdsOnce configured;
   hipError_t e = set_lds(k, lds, &configured);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(threads), lds, st, a);
@@ -67,7 +67,7 @@ template hipError_t launch_forward_blk<VW_T>(const FwdArgs<VW_T>&, int, int, boo
 template <typename T, int L, bool FMA, int NV>
 static hipError_t run_forward_persist(const FwdArgs<T>& a, int threads, int lds, hipStream_t st) {
   auto k = k_forward_persist<T, L, FMA, NV>;
-  static int configured = 64 * 1024;
+  static LdsOnce configured;
   hipError_t e = set_lds(k, lds, &configured);
   if (e != hipSuccess) return e;
   static int cus = 0;

@@ -2,6 +2,7 @@
 // (vw_capi.cpp).  Not installed; the public boundary is include/vectorwave_amd.h.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdint>
 
 namespace vw {
@@ -174,6 +175,29 @@ struct DenoiseConsts {
   int method;
   int n;
 };
+
+// Raise a kernel's dynamic-LDS limit past the 64 KiB default once per kernel instantiation AND
+// device (the attribute belongs to the device's copy of the function; a call per launch costs host
+// time).  `once` is a static of the caller, unique per kernel instantiation; several host threads
+// (one per context, vw_modwt_*_multi_f64) may race here -- the attribute call is idempotent and the
+// flag is atomic.
+constexpr int kMaxDevices = 64;
+struct LdsOnce {
+  std::atomic<int> limit[kMaxDevices];  // zero-initialised as a static: the 64 KiB default applies
+};
+template <typename Kern>
+static hipError_t set_lds(Kern k, int lds_bytes, LdsOnce* once, int want = kLdsBytes) {
+  if (lds_bytes <= 64 * 1024) return hipSuccess;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) dev = 0;
+  std::atomic<int>* f = dev < kMaxDevices ? &once->limit[dev] : nullptr;
+  if (f && f->load(std::memory_order_acquire) >= lds_bytes) return hipSuccess;
+  if (want < lds_bytes) want = lds_bytes;
+  hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, want);
+  if (e != hipSuccess) return e;
+  if (f) f->store(want, std::memory_order_release);
+  return hipSuccess;
+}
 
 // Launchers (vw_kernels.hip).  Return hipSuccess or the launch error.
 template <typename T>

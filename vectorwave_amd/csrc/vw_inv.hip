@@ -7,8 +7,7 @@ namespace vw {
 template <typename T, int L, bool FMA, int NV>
 static hipError_t run_inverse_fused_nv(const InvArgs<T>& a, int threads, int lds, hipStream_t st) {
   // pairwise sums: k_inverse_fused; sequential sums: two LDS buffers (k_inverse_db) or one (k_inverse_seq)
-  static int configured_pair = 64 * 1024, configured_seq = 64 * 1024, configured_db = 64 * 1024,
-             configured_blk = 64 * 1024;
+  static LdsOnce configured_pair, configured_seq, configured_db, configured_blk;
   // register-blocked PERIODIC (host contract; never with NV = 2)
   const bool blk = L > 0 && NV != 2 && a.blk && !a.pair && !a.db;
   auto k = a.pair ? k_inverse_fused<T, L, FMA, NV> : a.db ? k_inverse_db<T, L, FMA, NV> : k_inverse_seq<T, L, FMA, NV>;

@@ -17,17 +17,5 @@ namespace vw {
 #define VW_TAP_LIST(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(24) X(30)
 #endif
 
-// Raise the dynamic-LDS limit once per kernel instantiation (a call per launch costs host time).
-// `configured` must be a static of the caller, which is unique per kernel instantiation.
-template <typename Kern>
-static hipError_t set_lds(Kern k, int lds_bytes, int* configured) {
-  if (lds_bytes > *configured) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       kLdsBytes);
-    if (e != hipSuccess) return e;
-    *configured = kLdsBytes;
-  }
-  return hipSuccess;
-}
 
 }  // namespace vw

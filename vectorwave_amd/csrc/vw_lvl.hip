@@ -8,13 +8,13 @@ static hipError_t run_level(const LevelArgs<T>& a, int lds, hipStream_t st) {
   const unsigned tiles = (unsigned)((a.N + a.tile - 1) / a.tile);
   if constexpr (INV) {
     auto k = k_inverse_level<T, L, FMA>;
-    static int configured = 64 * 1024;
+    static LdsOnce configured;
   hipError_t e = set_lds(k, lds, &configured);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(tiles, (unsigned)a.B), dim3(256), lds, st, a);
   } else {
     auto k = k_forward_level<T, L, FMA>;
-    static int configured = 64 * 1024;
+    static LdsOnce configured;
   hipError_t e = set_lds(k, lds, &configured);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k, dim3(tiles, (unsigned)a.B), dim3(256), lds, st, a);

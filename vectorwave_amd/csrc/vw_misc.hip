@@ -13,18 +13,6 @@ namespace vw {
 #define VW_TAP_LIST(X) X(2) X(4) X(6) X(8) X(10) X(12) X(14) X(16) X(18) X(20) X(24) X(30)
 #endif
 
-// Raise the dynamic-LDS limit once per kernel instantiation (a call per launch costs host time).
-// `configured` must be a static of the caller, which is unique per kernel instantiation.
-template <typename Kern>
-static hipError_t set_lds(Kern k, int lds_bytes, int* configured) {
-  if (lds_bytes > *configured) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       kLdsBytes);
-    if (e != hipSuccess) return e;
-    *configured = kLdsBytes;
-  }
-  return hipSuccess;
-}
 
 bool has_unrolled_taps(int L) {
   switch (L) {
@@ -102,13 +90,9 @@ hipError_t launch_level_threshold(const double* coeffs, long long level_stride, 
     int npow2 = 1;
     while (npow2 < k.n) npow2 <<= 1;
     const int lds = npow2 * (int)sizeof(unsigned long long);
-    static int configured = 64 * 1024;  // (this kernel also has static LDS: raise the limit to what it asks)
-    if (lds > configured) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(k_sure_threshold),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-      if (e != hipSuccess) return e;
-      configured = lds;
-    }
+    static LdsOnce configured;  // (this kernel also has static LDS: raise the limit to what it asks)
+    hipError_t e = set_lds(k_sure_threshold, lds, &configured, lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_sure_threshold, grid, dim3(kSureThreads), lds, st, coeffs, level_stride, sigma, k, B, thr);
   } else {
     hipLaunchKernelGGL(k_level_threshold, grid, dim3(64), 0, st, coeffs, level_stride, sigma, k, B, thr);

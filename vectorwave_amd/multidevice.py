@@ -9,8 +9,9 @@ host thread, with no exchange between devices.
 * Host arrays (numpy, the JNI/FFM caller's ``double[][]``): one C call,
   ``vw_modwt_forward_multi_f64`` / ``vw_modwt_inverse_multi_f64``, whose std::threads stage each
   block through its own context.
-* Device tensors (one per context, already on that context's device): one Python thread per context
-  calling that context's engine.
+* Device tensors (one per context, already on that context's device): one C call,
+  ``vw_modwt_forward_multi_dev_f64`` / ``vw_modwt_inverse_multi_dev_f64``, whose std::threads enqueue
+  each shard on its own context's stream -- no staging, nothing crosses PCIe.
 
 Contexts may share a device (several ``Engine`` instances on cuda:0 -- what the tests do on a one-GPU
 box) or sit on different devices.
@@ -18,7 +19,6 @@ box) or sit on different devices.
 from __future__ import annotations
 
 import ctypes
-from concurrent.futures import ThreadPoolExecutor
 from ctypes import c_void_p
 from typing import List, Optional, Sequence
 
@@ -86,18 +86,60 @@ class DeviceGroup:
                                                      0xFFFFFFFF, 0, flags, y.ctypes.data_as(c_void_p)))
         return y
 
-    # -- device tensors: one Python thread per context ------------------------------------------
-    def forward_device(self, xs, wavelet: Wavelet, levels: int, boundary: int = nat.PERIODIC, fma: bool = False):
-        """xs: one [B_k][N] CUDA tensor per context (on that context's device) -> [(details, approx)]."""
+    # -- device tensors: one C call, one std::thread per context, no staging ----------------------
+    def _dev_ptrs(self, ts):
+        return (c_void_p * len(self.engines))(*[t.data_ptr() for t in ts])
+
+    def _sync_devices(self):
+        import torch
+        for d in sorted({e.device for e in self.engines}):
+            torch.cuda.synchronize(d)
+
+    def forward_device(self, xs, wavelet: Wavelet, levels: int, boundary: int = nat.PERIODIC, fma: bool = False,
+                       core_levels: bool = False):
+        """xs: one [B_k][N] float64 CUDA tensor per context, on that context's device (a batch already
+        sharded across GPUs) -> [(details [J][B_k][N], approx [B_k][N])], allocated on the same devices.
+        One ``vw_modwt_forward_multi_dev_f64`` call: context k's host thread enqueues its shard on its own
+        stream, nothing crosses PCIe; returns when every shard is done."""
+        import torch
         if len(xs) != len(self.engines):
             raise InvalidArgumentException("one tensor per context")
+        xs = [x.contiguous() for x in xs]
+        N = xs[0].shape[-1]
+        for k, x in enumerate(xs):
+            if x.dtype != torch.float64 or x.ndim != 2 or x.shape[1] != N or not x.is_cuda \
+                    or x.device.index != self.engines[k].device:
+                raise InvalidArgumentException(f"xs[{k}] must be a [rows][{N}] float64 tensor on cuda:"
+                                               f"{self.engines[k].device}")
+        outs = [(torch.empty((levels, x.shape[0], N), dtype=torch.float64, device=x.device),
+                 torch.empty_like(x)) for x in xs]
+        rows = (ctypes.c_int64 * len(xs))(*[x.shape[0] for x in xs])
         lo, hi = wavelet.lowPassDecomposition(), wavelet.highPassDecomposition()
-        fl = nat.FLAG_FMA if fma else 0
+        flags = nat.FLAG_SYNC | (nat.FLAG_FMA if fma else 0) | (nat.FLAG_CORE_LEVELS if core_levels else 0)
+        self._sync_devices()  # the inputs were written on torch's streams
+        _check(nat.load().vw_modwt_forward_multi_dev_f64(
+            self._ctxs, len(xs), self._dev_ptrs(xs), rows, N, N, nat.taps_array(lo), nat.taps_array(hi), len(lo),
+            wavelet.wavelet_id, boundary, levels, flags, self._dev_ptrs([d for d, _ in outs]),
+            self._dev_ptrs([a for _, a in outs])))
+        return outs
 
-        def one(k):
-            return self.engines[k].forward(xs[k], lo, hi, wavelet.wavelet_id, boundary, levels, fl)
-        with ThreadPoolExecutor(max_workers=len(self.engines)) as ex:
-            return list(ex.map(one, range(len(self.engines))))
+    def inverse_device(self, parts, wavelet: Wavelet, boundary: int = nat.PERIODIC, fma: bool = False):
+        """parts: [(details [J][B_k][N], approx [B_k][N])] per context, on its device -> [y [B_k][N]]."""
+        import torch
+        if len(parts) != len(self.engines):
+            raise InvalidArgumentException("one (details, approx) pair per context")
+        parts = [(d.contiguous(), a.contiguous()) for d, a in parts]
+        J, _, N = parts[0][0].shape
+        ys = [torch.empty_like(a) for _, a in parts]
+        rows = (ctypes.c_int64 * len(parts))(*[a.shape[0] for _, a in parts])
+        lo, hi = wavelet.lowPassReconstruction(), wavelet.highPassReconstruction()
+        flags = nat.FLAG_SYNC | (nat.FLAG_FMA if fma else 0)
+        self._sync_devices()
+        _check(nat.load().vw_modwt_inverse_multi_dev_f64(
+            self._ctxs, len(parts), self._dev_ptrs([d for d, _ in parts]), self._dev_ptrs([a for _, a in parts]),
+            rows, N, nat.taps_array(lo), nat.taps_array(hi), len(lo), wavelet.wavelet_id, boundary, J, 0xFFFFFFFF,
+            0, flags, self._dev_ptrs(ys)))
+        return ys
 
     def close(self) -> None:
         if self._own:
