@@ -41,10 +41,31 @@ from ctypes import c_void_p
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-ACC_NAME = {
-    True: "fma (fused multiply-add per tap; max-abs error vs vectorwave-core < 1e-12 at this configuration, tests/test_gpu_headline.py)",
-    False: "exact (separate multiply and add in the reference's tap order; bit-identical to vectorwave-core)",
+# The accumulation claim of each config's line, naming the test and the tolerance that cover it.
+ACC_FMA = {
+    "db4": "fma (fused multiply-add per tap; max-abs error vs vectorwave-core <= 1e-12 at this configuration, "
+           "4096 x 4096 in the bench's own kernel policy: tests/test_gpu_headline.py)",
+    "sym8-denoise": "fma (fused multiply-add per tap; output within 1e-12 * max|x| and thresholds within 1e-12 "
+                    "relative of vectorwave-core at the config-3 shape sym8 J=8 N=16384: "
+                    "tests/test_gpu_configs.py::test_config3_sym8_swt_j8_denoise_16384)",
+    "db8-stream": "fma (fused multiply-add per tap; every level, approximation and inverse within 1e-12 of "
+                  "vectorwave-extensions' BatchMODWT on a db8 J=10 2^20 block: "
+                  "tests/test_gpu_configs.py::test_config4_db8_j10_block_2p20)",
+    "coif5-f32": "fma fp32 (fused multiply-add per tap in fp32; within 1e-5 * max|x| * J of the fp64 "
+                 "restatement, SURVEY.md §8d: tests/test_gpu_configs.py::test_config5_coif5_f32_j6_8192)",
 }
+ACC_EXACT = {
+    "db4": "exact (separate multiply and add in the reference's tap order; bit-identical to vectorwave-core: "
+           "tests/test_gpu_headline.py, tests/test_gpu_parity.py)",
+    "sym8-denoise": "exact (bit-identical output and thresholds: tests/test_gpu_configs.py)",
+    "db8-stream": "exact (bit-identical in all 10 levels and the inverse: tests/test_gpu_configs.py)",
+    "coif5-f32": "exact fp32 (separate multiply and add in fp32; within 1e-5 * max|x| * J of the fp64 "
+                 "restatement: tests/test_gpu_configs.py)",
+}
+
+
+def acc_name(config, fma):
+    return (ACC_FMA if fma else ACC_EXACT).get(config, "fma" if fma else "exact")
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (/opt/skills/guides/MI355X_MICROARCH.md)
 # Vector-ALU peaks for the FMA work of the taps: fp32 from the microarchitecture guide (157.3 TFLOP/s
 # vector), fp64 the MI355X spec sheet's 78.6 (the guide lists no fp64 figure); beside them the issue
@@ -688,7 +709,7 @@ def run(args, world, rank, local):
         (ael, _), _, afams, asampled, _ = measure(torch, dist, world, wl, aflags, args.launch, args.steps,
                                                   args.warmup, min(args.settle, 0.3), events)
         ael = max_over_ranks(torch, dist, world, ael, dev)
-        alt = {"accumulation": ACC_NAME[bool(aflags & nat.FLAG_FMA)],
+        alt = {"accumulation": acc_name(args.config, bool(aflags & nat.FLAG_FMA)),
                "value": round(Bg * N * args.steps / ael / 1e6, 2),
                "kernels_ms": {k: round(ms / n, 5) for k, (ms, n) in afams.items()}}
     wl.close()
@@ -734,7 +755,7 @@ def run(args, world, rank, local):
             "config": {
                 "workload": f"{wname} MODWT J={J} {pipeline}, global batch {Bg} x {N} samples, {dtype}, PERIODIC",
                 "wavelet": wname, "levels": J, "global_batch": Bg, "batch_per_gpu": rows, "signal_length": N,
-                "boundary": "PERIODIC", "accumulation": ACC_NAME[bool(flags & nat.FLAG_FMA)],
+                "boundary": "PERIODIC", "accumulation": acc_name(args.config, bool(flags & nat.FLAG_FMA)),
                 "parallelism": f"batch-shard x{world} (contiguous row blocks, no collective)"
                                + (f", {K} contexts per GPU (own stream each, row blocks)" if K > 1 else ""),
                 "contexts_per_gpu": K,

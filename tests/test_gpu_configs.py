@@ -156,3 +156,95 @@ def test_config5_coif5_f32_j6_8192(engine):
         y_ref = O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC)
         np.testing.assert_allclose(y[b], y_ref, rtol=0, atol=tol)
     assert np.max(np.abs(y - x32)) < 1e-3  # coif5's truncated taps + fp32
+
+
+# ---- full BASELINE batch sizes: the kernel policy sees the real batch, so a policy that
+# switches with B (two-buffer inverse at small batches, NV = 2, persistent grids) is exercised exactly as
+# bench.py runs it.  Inputs as bench.py's (counter-based uniform, generated on device), C-ABI calls on
+# device buffers; first / middle / last rows against the restatement.
+def _full_rows(B):
+    return (0, B // 2 - 1, B - 1)
+
+
+@pytest.mark.parametrize("fma", [False, True], ids=["exact", "fma"])
+def test_config3_full_batch_16384x16384(engine, fma):
+    import torch
+    from ctypes import c_void_p
+    from vectorwave_amd import _native as nat
+    w = Symlet.SYM8
+    n, J, B = 16384, 8, 16384
+    x = torch.empty((B, n), dtype=torch.float64, device="cuda")
+    engine.fill_uniform(x, 42)
+    y = torch.empty_like(x)
+    thr = torch.empty((B,), dtype=torch.float64, device="cuda")
+    lo, hi = lohi(w)
+    P = lambda t: c_void_p(t.data_ptr())  # noqa: E731
+    engine.bind_torch_stream()
+    st = engine.lib.vw_swt_denoise_f64(engine.ctx, P(x), B, n, n, nat.taps_array(lo), nat.taps_array(hi), len(lo),
+                                       w.wavelet_id, nat.PERIODIC, J, -1.0, 1, nat.FLAG_FMA if fma else 0, P(y),
+                                       P(thr))
+    assert st == 0, nat.last_error()
+    torch.cuda.synchronize()
+    for b in _full_rows(B):
+        xr = x[b].cpu().numpy()
+        y_ref, t_ref = O.swt_denoise(xr, lo, hi, O.PERIODIC, J, -1.0, True, wavelet_id=w.wavelet_id)
+        if fma:
+            assert abs(thr[b].item() - t_ref) <= 1e-12 * abs(t_ref)
+            np.testing.assert_allclose(y[b].cpu().numpy(), y_ref, rtol=0, atol=1e-12 * np.max(np.abs(xr)))
+        else:
+            assert thr[b].item() == t_ref
+            exact(y[b].cpu().numpy(), y_ref, f"denoised signal {b}")
+    del x, y
+
+
+def test_config5_full_batch_65536x8192_f32(engine):
+    import torch
+    from ctypes import c_void_p
+    from vectorwave_amd import _native as nat
+    w = Coiflet.COIF5
+    n, J, B = 8192, 6, 65536
+    x = torch.empty((B, n), dtype=torch.float32, device="cuda")
+    engine.fill_uniform(x, 42)
+    det = torch.empty((J, B, n), dtype=torch.float32, device="cuda")
+    app = torch.empty_like(x)
+    y = torch.empty_like(x)
+    lo, hi = lohi(w)
+    la, ha = nat.taps_array(lo), nat.taps_array(hi)
+    P = lambda t: c_void_p(t.data_ptr())  # noqa: E731
+    engine.bind_torch_stream()
+    lib = engine.lib
+    assert lib.vw_modwt_forward_f32(engine.ctx, P(x), B, n, n, la, ha, len(lo), w.wavelet_id, nat.PERIODIC, J,
+                                    nat.FLAG_FMA, P(det), P(app)) == 0, nat.last_error()
+    assert lib.vw_modwt_inverse_f32(engine.ctx, P(det), P(app), B, n, la, ha, len(lo), w.wavelet_id, nat.PERIODIC,
+                                    J, 0xFFFFFFFF, 0, nat.FLAG_FMA, P(y)) == 0, nat.last_error()
+    torch.cuda.synchronize()
+    for b in _full_rows(B):
+        xr = x[b].double().cpu().numpy()
+        tol = 1e-5 * float(np.max(np.abs(xr))) * J
+        d_ref, a_ref = O.decompose(xr, lo, hi, O.PERIODIC, J)
+        y_ref = O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC)
+        np.testing.assert_allclose(det[:, b, :].double().cpu().numpy(), d_ref, rtol=0, atol=tol)
+        np.testing.assert_allclose(app[b].double().cpu().numpy(), a_ref, rtol=0, atol=tol)
+        np.testing.assert_allclose(y[b].double().cpu().numpy(), y_ref, rtol=0, atol=tol)
+    del x, det, app, y
+
+
+@pytest.mark.parametrize("chunk", [64, 3])
+def test_multi_level_tiles_xcd_runs_identical(engine, chunk):
+    """VW_MULTI_XCD (vw_device.h multi_work): the multi-level tile kernels on a 1-D grid of XCD runs of
+    neighbouring tiles, padding workgroups included (3 signals x 128 tiles is not a multiple of 8 runs):
+    the same outputs bit for bit as the 2-D grid, forward and inverse, EXACT and FMA."""
+    import torch
+    w = Daubechies.DB8
+    n, J, B = 1 << 18, 10, 3
+    x = torch.empty((B, n), dtype=torch.float64, device="cuda")
+    engine.fill_uniform(x, 7)
+    for fma in (False, True):
+        m0 = vw.BatchMODWT.multiLevelAoS(w, x, J, fma=fma)
+        y0 = vw.BatchMODWT.inverseMultiLevelAoS(w, m0.detailPerLevel, m0.finalApprox, fma=fma)
+        with engine.options(VW_MULTI_XCD=chunk):
+            m1 = vw.BatchMODWT.multiLevelAoS(w, x, J, fma=fma)
+            y1 = vw.BatchMODWT.inverseMultiLevelAoS(w, m1.detailPerLevel, m1.finalApprox, fma=fma)
+        torch.cuda.synchronize()
+        assert torch.equal(m0.detailPerLevel, m1.detailPerLevel) and torch.equal(m0.finalApprox, m1.finalApprox)
+        assert torch.equal(y0, y1)

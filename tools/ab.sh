@@ -1,5 +1,6 @@
 #!/bin/bash
 # Same-box A/B driver for bench.py variants, alternating REPS times (one fresh process per run).
+# Library variants: VW_LIB_PATH=build/var_NAME/libvectorwave_amd.so in the env part (tools/build_variant.sh).
 #   V='ENV=1 ENV2=x|--args;|--other args' CFG=db4 STEPS=20 REPS=3 OUT=gpurun_out/ab_x.log bash tools/ab.sh
 # A variant is "<env assignments>|<bench arguments>" (either side may be empty).  Each run prints one
 # log line: the variant, value, per-pass ms, check ok.  A crash / timeout stops the script (no retry).

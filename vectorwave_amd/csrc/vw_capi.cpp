@@ -71,10 +71,12 @@ struct Tuning {
   int fwd_buf = 0;         // VW_FWD_BUF=1|2: force one / two forward level buffers (0 = policy)
   bool force_tiled = false;// VW_FORCE_TILED: per-level path even when the fused kernels fit
   int fwd_rev = 0, inv_rev = 0;  // VW_FWD_REV / VW_INV_REV: reverse workgroup -> signal walk
+  int inv_persist = 0;           // VW_INV_PERSIST=1: persistent two-region inverse (k_inverse_persist)
   int fwd_tile = 0;        // VW_FWD_TILE: per-level forward tile (0 = default)
   bool multi = true;       // VW_MULTI=0: one launch per level on the long-signal path
   int multi_div = 4;       // VW_MULTI_DIV: reach bound of a level group = tile / div
   int multi_tile = 0;      // VW_MULTI_TILE: multi-level tile (0 = 16 KiB of samples)
+  int multi_xcd = 0;       // VW_MULTI_XCD: runs of this many neighbouring tiles per XCD (0 = 2-D grid)
   int inv_buf = 0;         // VW_INV_BUF=2: two-buffer sequential inverse (k_inverse_db)
   int inv_tile = 0;        // VW_INV_TILE: per-level inverse tile (0 = 1024)
   int multi_rblk = 1;      // VW_MULTI_RBLK: register-blocked taps in k_inverse_multi
@@ -115,10 +117,12 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_FORCE_TILED") t.force_tiled = v > 0;
   else if (k == "VW_FWD_REV") t.fwd_rev = v < 0 ? 0 : v;
   else if (k == "VW_INV_REV") t.inv_rev = v < 0 ? 0 : v;
+  else if (k == "VW_INV_PERSIST") t.inv_persist = v < 0 ? d.inv_persist : v;
   else if (k == "VW_FWD_TILE") t.fwd_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI") t.multi = v < 0 ? d.multi : v != 0;
   else if (k == "VW_MULTI_DIV") t.multi_div = v <= 0 ? d.multi_div : v;
   else if (k == "VW_MULTI_TILE") t.multi_tile = v < 0 ? 0 : v;
+  else if (k == "VW_MULTI_XCD") t.multi_xcd = v < 0 ? d.multi_xcd : v;
   else if (k == "VW_INV_BUF") t.inv_buf = v < 0 ? 0 : v;  // 0 = policy
   else if (k == "VW_INV_TILE") t.inv_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI_RBLK") t.multi_rblk = v < 0 ? d.multi_rblk : v;
@@ -152,7 +156,8 @@ static const char* const kTuningKeys[] = {
     "VW_FWD_TILE", "VW_MULTI", "VW_MULTI_DIV", "VW_MULTI_TILE", "VW_INV_BUF", "VW_INV_TILE", "VW_MULTI_RBLK", "VW_MULTI_PF", "VW_MULTI_PAD", "VW_MULTI_INV_TILE", "VW_NO_SWEEP", "VW_SWEEP_QC",
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
-    "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8"};
+    "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8",
+    "VW_INV_PERSIST", "VW_MULTI_XCD"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -1131,6 +1136,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
         m.region = (int)round_up(m.ext[0] + mtile + V, V);
         m.vec_io = (N % V == 0) && (lda % V == 0) && al;
         m.taps = L;
+        m.xcd_chunk = tu.multi_xcd;
         copy_taps(m.lo, lo, L);
         copy_taps(m.hi, hi, L);
         {
@@ -1257,7 +1263,32 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   bool fused = false, fit = false;
   const bool inv_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
   const int inv_nv2 = (tu.inv_nv == 2 && inv_io && L <= 8 && L <= tu.unroll_max && has_unrolled_taps(L)) ? 2 : 0;
-  if (!tu.force_tiled) {
+  // Persistent two-region inverse (vw_device.h k_inverse_persist): two LDS regions of N + right halo
+  // (rounded to whole 64-vector DMA instructions), rows by LDS-DMA, the resident grid walks the batch.
+  // Contract: PERIODIC sequential sums, every detail level and the approximation present, no
+  // thresholds, aligned rows, short unrolled filters, full slabs of whole waves.
+  bool persist = false;
+  int64_t dma_vec = 0;
+  const unsigned all_levels = J >= 32 ? 0xFFFFFFFFu : ((1u << J) - 1u);
+  if (tu.inv_persist && !tu.force_tiled && !pair && boundary == VW_PERIODIC && !approx_zero && !thr &&
+      (detail_mask & all_levels) == all_levels && inv_io && L <= 8 && L <= tu.unroll_max && has_unrolled_taps(L) &&
+      max_hl == 0 && nvec % 64 == 0) {
+    const int pnv = inv_nv2 ? 2 : 4;
+    const int64_t hvec = round_up((max_hr + V - 1) / V, 64);
+    const int64_t th = nvec / pnv;
+    const int64_t bytes = 2 * (nvec + hvec) * V * (int64_t)sizeof(T);
+    if (hvec <= nvec && th % 64 == 0 && th <= (pnv == 2 ? 1024 : 512) && bytes <= kLdsBytes / 2) {
+      persist = true;
+      fused = true;
+      fit = true;
+      db = false;
+      dma_vec = nvec + hvec;
+      nv = pnv;
+      threads = (int)th;
+      lds = (int)bytes;
+    }
+  }
+  if (!persist && !tu.force_tiled) {
     if (pair || db) fused = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit, inv_nv2);
     if (!fused && !pair) {
       db = false;
@@ -1271,12 +1302,17 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     a.details = details; a.approx = approx; a.y = y; a.B = B; a.N = (int)N; a.J = J;
     a.db = db ? 1 : 0;
     a.hlpad_a = hlpad; a.hlpad_d = hlpad; a.region_d = (int)region;
+    if (persist) {
+      a.persist = 1;
+      a.dma_vec = (int)dma_vec;
+      a.region_d = (int)(dma_vec * V);
+    }
     a.vec_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
     a.unrolled = a.vec_io && fit && L <= tu.unroll_max;
     a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.thr_ld = thr_ld; a.soft = soft; a.taps = L;
     a.rev = tu.inv_rev;
     // register-blocked PERIODIC inverse for long filters (vw_device.h k_inverse_blk)
-    if (tu.blk > 0 && L >= tu.blk && nv != 2 && !pair && !db && boundary == VW_PERIODIC && a.unrolled &&
+    if (tu.blk > 0 && L >= tu.blk && nv != 2 && !pair && !db && !persist && boundary == VW_PERIODIC && a.unrolled &&
         (int64_t)threads * nv == nvec) {
       bool okb = true;
       int64_t buf = 0;
@@ -1383,6 +1419,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         m.region = (int)round_up(mtile + m.ext[g - 1] + V, V);
         m.vec_io = (N % V == 0) && al;
         m.soft = soft; m.taps = L;
+        m.xcd_chunk = tu.multi_xcd;
         m.rblk = tu.multi_rblk;
         // register prefetch of d_{j-1} while level j computes: whole vectors, every tile of the group
         m.pf = tu.multi_pf && m.vec_io && (int64_t)(mtile + m.ext[g - 1]) / V <= (int64_t)kMultiPF * 256;

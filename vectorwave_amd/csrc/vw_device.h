@@ -819,6 +819,77 @@ __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
+// vmcnt(n) for a wave-uniform runtime n (0..63; larger waits for 63, i.e. for more)
+__device__ __forceinline__ void wait_vmcnt_rt(int n) {
+  switch (n) {
+    case 0: wait_vmcnt<0>(); break;
+    case 1: wait_vmcnt<1>(); break;
+    case 2: wait_vmcnt<2>(); break;
+    case 3: wait_vmcnt<3>(); break;
+    case 4: wait_vmcnt<4>(); break;
+    case 5: wait_vmcnt<5>(); break;
+    case 6: wait_vmcnt<6>(); break;
+    case 7: wait_vmcnt<7>(); break;
+    case 8: wait_vmcnt<8>(); break;
+    case 9: wait_vmcnt<9>(); break;
+    case 10: wait_vmcnt<10>(); break;
+    case 11: wait_vmcnt<11>(); break;
+    case 12: wait_vmcnt<12>(); break;
+    case 13: wait_vmcnt<13>(); break;
+    case 14: wait_vmcnt<14>(); break;
+    case 15: wait_vmcnt<15>(); break;
+    case 16: wait_vmcnt<16>(); break;
+    case 17: wait_vmcnt<17>(); break;
+    case 18: wait_vmcnt<18>(); break;
+    case 19: wait_vmcnt<19>(); break;
+    case 20: wait_vmcnt<20>(); break;
+    case 21: wait_vmcnt<21>(); break;
+    case 22: wait_vmcnt<22>(); break;
+    case 23: wait_vmcnt<23>(); break;
+    case 24: wait_vmcnt<24>(); break;
+    case 25: wait_vmcnt<25>(); break;
+    case 26: wait_vmcnt<26>(); break;
+    case 27: wait_vmcnt<27>(); break;
+    case 28: wait_vmcnt<28>(); break;
+    case 29: wait_vmcnt<29>(); break;
+    case 30: wait_vmcnt<30>(); break;
+    case 31: wait_vmcnt<31>(); break;
+    case 32: wait_vmcnt<32>(); break;
+    case 33: wait_vmcnt<33>(); break;
+    case 34: wait_vmcnt<34>(); break;
+    case 35: wait_vmcnt<35>(); break;
+    case 36: wait_vmcnt<36>(); break;
+    case 37: wait_vmcnt<37>(); break;
+    case 38: wait_vmcnt<38>(); break;
+    case 39: wait_vmcnt<39>(); break;
+    case 40: wait_vmcnt<40>(); break;
+    case 41: wait_vmcnt<41>(); break;
+    case 42: wait_vmcnt<42>(); break;
+    case 43: wait_vmcnt<43>(); break;
+    case 44: wait_vmcnt<44>(); break;
+    case 45: wait_vmcnt<45>(); break;
+    case 46: wait_vmcnt<46>(); break;
+    case 47: wait_vmcnt<47>(); break;
+    case 48: wait_vmcnt<48>(); break;
+    case 49: wait_vmcnt<49>(); break;
+    case 50: wait_vmcnt<50>(); break;
+    case 51: wait_vmcnt<51>(); break;
+    case 52: wait_vmcnt<52>(); break;
+    case 53: wait_vmcnt<53>(); break;
+    case 54: wait_vmcnt<54>(); break;
+    case 55: wait_vmcnt<55>(); break;
+    case 56: wait_vmcnt<56>(); break;
+    case 57: wait_vmcnt<57>(); break;
+    case 58: wait_vmcnt<58>(); break;
+    case 59: wait_vmcnt<59>(); break;
+    case 60: wait_vmcnt<60>(); break;
+    case 61: wait_vmcnt<61>(); break;
+    case 62: wait_vmcnt<62>(); break;
+    case 63: wait_vmcnt<63>(); break;
+    default: wait_vmcnt<63>(); break;
+  }
+}
+
 template <typename T, int L, bool FMA, int NV>
 __global__ void __attribute__((amdgpu_flat_work_group_size(1, NV <= 4 ? 512 : 1024), amdgpu_waves_per_eu(4)))
 k_forward_persist(const FwdArgs<T> p) {
@@ -1022,6 +1093,100 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, VW_INV_W)) k_inverse_seq(const
     }
   }
   for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, w * V, N, vec_ok, acc[k]); });
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent two-region inverse (PERIODIC K4, sequential sums: MultiLevelMODWTTransform.java:576-589,
+// VectorWaveSwtAdapter.reconstructPeriodic :444-474).  Region Q holds a_j, region P holds d_j, both
+// with their periodic right halo.  The detail rows and each signal's a_J arrive by LDS-DMA
+// (global_load_lds_dwordx4: no VGPRs, so no 16-register prefetch row), each level is
+//   barrier -> approx branch (reads Q) -> wait own DMA of d_j, barrier -> detail branch (reads P)
+//   -> barrier -> DMA d_{j-1} into P, a_{j-1} (registers) into Q with its halo images
+// i.e. three barriers instead of k_inverse_seq's four, and d_{j-1}'s DMA lands while the approximation
+// branch of the next level computes.  The resident grid walks the batch (b = blockIdx.x + k*gridDim.x);
+// during level 1 the next signal's a_J goes into Q as soon as the approximation branch has read it
+// (overlapping the detail branch and the y stores) and its d_J into P after the detail branch, so no
+// signal starts with an exposed row load.  Per output the approximation taps then the detail taps,
+// l ascending: bit-exact in EXACT mode.
+//
+// Host contract (vw_capi.cpp inverse_impl): PERIODIC, every detail level present, approximation
+// present, no thresholds, aligned rows, full slabs (threads * NV == N / V), whole waves, and
+// dma_vec = N / V + right-halo vectors rounded up to 64 (one wave instruction = 64 x 16 B; the halo
+// vectors re-read the row's first vectors, v - N/V).
+// DMA wave-instructions this wave issues for a row of tvec vectors (dma_row_periodic's loop count)
+__device__ __forceinline__ int dma_count(int tvec) {
+  const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6, nc = tvec / 64;
+  return wv < nc ? (nc - wv + nw - 1) / nw : 0;
+}
+
+template <typename T>
+__device__ __forceinline__ int dma_row_periodic(T* buf, const T* __restrict__ src, int nvec, int tvec) {
+  constexpr int V = VT<T>::V;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  int n = 0;
+  for (int c = wv; c * 64 < tvec; c += nw, ++n) {
+    int v = c * 64 + lane;
+    v = v < nvec ? v : v - nvec;
+    const T* g = src + (size_t)v * V;
+    const unsigned lds = (unsigned)(uintptr_t)(buf + c * 64 * V);  // LDS byte address (wave-uniform)
+    unsigned keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
+        : "memory");
+  }
+  return n;
+}
+
+template <typename T, int L, bool FMA, int NV>
+__global__ void __attribute__((amdgpu_flat_work_group_size(1, NV == 2 ? 1024 : 512),
+                               amdgpu_waves_per_eu(NV == 2 ? 8 : 4)))
+k_inverse_persist(const InvArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* const Q = reinterpret_cast<T*>(smem);               // a_j + halo
+  T* const P = reinterpret_cast<T*>(smem) + p.region_d;  // d_j + halo
+  const int N = p.N;
+  const int nvec = N / V;
+  const int tvec = p.dma_vec;
+  const int J = p.J;
+  const long long G = gridDim.x;
+  const size_t plane = (size_t)p.B * (size_t)N;
+  long long b = blockIdx.x;
+  if (b >= p.B) return;
+  dma_row_periodic<T>(Q, p.approx + b * (size_t)N, nvec, tvec);
+  dma_row_periodic<T>(P, p.details + (size_t)(J - 1) * plane + b * (size_t)N, nvec, tvec);
+  wait_vmcnt_rt(dma_count(tvec));  // a_J landed (d_J may still be in flight)
+  for (;;) {
+    const long long bn = b + G;
+    T acc[NV][V];
+    for (int j = J; j >= 1; --j) {
+      const LevelDesc lv = p.lv[j - 1];
+      lds_barrier();  // Q = a_j + halo; every read of the previous level done
+      zero_regs<T, NV>(acc);
+      inv_row<T, L, FMA, NV>(Q, nvec, lv.s, lv.dir_a, lv.off_a, p.lo, p.taps, acc);
+      wait_vmem();    // this wave's share of d_j (the only vector-memory operations in flight but stores)
+      lds_barrier();  // P = d_j + halo; every read of Q done
+      if (j == 1 && bn < p.B) dma_row_periodic<T>(Q, p.approx + bn * (size_t)N, nvec, tvec);  // next a_J
+      inv_row<T, L, FMA, NV>(P, nvec, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
+      if (j > 1) {
+        lds_barrier();  // every read of P done
+        dma_row_periodic<T>(P, p.details + (size_t)(j - 2) * plane + b * (size_t)N, nvec, tvec);
+        regs_to_level<T, L, NV>(Q, acc, nvec, N, p.lv[j - 2], 0, (const T*)nullptr);
+      }
+    }
+    for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, w * V, N, true, acc[k]); });
+    if (bn >= p.B) break;
+    lds_barrier();  // every read of P (level 1's detail branch) done
+    const int nd = dma_row_periodic<T>(P, p.details + (size_t)(J - 1) * plane + bn * (size_t)N, nvec, tvec);
+    wait_vmcnt_rt(NV + nd);  // the next a_J landed; the y stores and the d_J DMA stay in flight
+    b = bn;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2056,6 +2221,28 @@ __global__ void __launch_bounds__(12 * R) k_inverse_sweep3(const LevelArgs<T> p)
 // (ScalarOps.java:700-723 reads t - l*s), to the right in the inverse (MultiLevelMODWTTransform
 // .java:576-589 reads t + l*s).  The redundant ext/tile of the arithmetic buys one HBM round trip
 // per group instead of one per level.
+// Workgroup -> (signal b, tile t) of the multi-level tile kernels.  xcd_chunk C = 0: the 2-D grid
+// (tiles, signals).  C > 0: a 1-D grid rounded up to 8C; the tiles in signal-major order (u = b * tiles
+// + t) are cut into runs of C neighbours, run k going to the XCD of workgroups k mod 8 (dispatch deals
+// workgroups round-robin over the 8 XCDs: g and g + 8 share one), each XCD taking its runs in order.
+// Neighbouring tiles, whose reaches overlap, then run on one XCD close in time, so the reach a tile
+// re-reads was just brought into that XCD's L2 by its neighbour instead of coming from HBM again.
+// Placement is a speed hint only: any order computes the same outputs.
+__device__ __forceinline__ bool multi_work(int tiles, long long B, int C, long long* b, int* t) {
+  if (C <= 0) {
+    *b = blockIdx.y;
+    *t = blockIdx.x;
+    return true;
+  }
+  const long long id = blockIdx.x;
+  const long long xcd = id & 7, slot = id >> 3;
+  const long long u = ((slot / C) * 8 + xcd) * C + slot % C;
+  if (u >= B * (long long)tiles) return false;
+  *b = u / tiles;
+  *t = (int)(u % tiles);
+  return true;
+}
+
 template <typename T, int L, bool FMA>
 __global__ void __launch_bounds__(256) k_forward_multi(const MultiArgs<T> p) {
   constexpr int V = VT<T>::V;
@@ -2063,9 +2250,11 @@ __global__ void __launch_bounds__(256) k_forward_multi(const MultiArgs<T> p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* X = reinterpret_cast<T*>(smem) + p.ext[0];  // level input, positions [-ext[k], span)
   T* Y = X + p.region;
-  const long long b = blockIdx.y;
   const int N = p.N;
-  const int ts = blockIdx.x * p.tile;
+  long long b;
+  int tix;
+  if (!multi_work((N + p.tile - 1) / p.tile, p.B, p.xcd_chunk, &b, &tix)) return;
+  const int ts = tix * p.tile;
   const int cnt = min(p.tile, N - ts);
   const int span = (cnt + V - 1) / V * V;
   tile_to_lds(X, p.src_a + b * p.lda, N, ts, -p.ext[0], span, kHaloPeriodic, 0, (const T*)nullptr, 0,
@@ -2111,9 +2300,11 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* const A = reinterpret_cast<T*>(smem);  // positions [0, span + ext[k])
   T* const D = A + p.region;
-  const long long b = blockIdx.y;
   const int N = p.N;
-  const int ts = blockIdx.x * p.tile;
+  long long b;
+  int tix;
+  if (!multi_work((N + p.tile - 1) / p.tile, p.B, p.xcd_chunk, &b, &tix)) return;
+  const int ts = tix * p.tile;
   const int cnt = min(p.tile, N - ts);
   const int span = (cnt + V - 1) / V * V;
   const bool vec_ok = p.vec_io != 0;

@@ -92,6 +92,8 @@ struct InvArgs {
   int taps;
   int tap_lds;          // k_inverse_blk: element offset of the LDS tap table
   int blk_tight;        // k_inverse_blk: sparse padding (blk_layout)
+  int persist;          // 1: k_inverse_persist (two regions, LDS-DMA rows, resident grid walks the batch)
+  int dma_vec;          // k_inverse_persist: vectors per DMA'd row incl. the periodic right halo (x64)
   T lo[kMaxTaps];
   T hi[kMaxTaps];
   LevelDesc lv[kMaxLevels];
@@ -159,6 +161,7 @@ struct MultiArgs {
   int rblk;                  // inverse: register-blocked taps where S is a multiple of V
   int pf;                    // inverse: next level's detail tile prefetched into registers
   int pad;                   // inverse: padded LDS layout at the register-blocked levels (needs pf, rblk)
+  int xcd_chunk;             // > 0: 1-D grid, runs of xcd_chunk neighbouring tiles per XCD (multi_work)
   T lo[kMaxTaps];
   T hi[kMaxTaps];
 };

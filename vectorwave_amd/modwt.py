@@ -44,10 +44,25 @@ def _copy(a):
 
 
 def _energy(a) -> float:
+    """computeEnergy (MultiLevelMODWTResultImpl.java:211-216): ``energy += c * c`` in index order -- each
+    square rounded, then added to the running sum, left to right.  ``np.add.accumulate`` is that
+    sequential loop (a reduction like ``np.sum`` / ``np.dot`` would sum pairwise), so the value is the
+    reference's bit for bit.  A device tensor is read back first: energies are host-side scalars."""
     if _is_device_tensor(a):
-        return float((a.double() * a.double()).sum().item())
-    a = np.asarray(a, dtype=np.float64)
-    return float(np.dot(a.ravel(), a.ravel()))
+        a = a.detach().double().cpu().numpy()
+    a = np.asarray(a, dtype=np.float64).ravel()
+    if a.size == 0:
+        return 0.0
+    return float(np.add.accumulate(a * a)[-1])
+
+
+def _total_energy(res) -> float:
+    """getTotalEnergy (MultiLevelMODWTResultImpl.java:109-117): total = approximation energy, then
+    total += the detail energy of level 1, 2, ..., J."""
+    total = res.getApproximationEnergy()
+    for j in range(1, res.getLevels() + 1):
+        total += res.getDetailEnergyAtLevel(j)
+    return total
 
 
 def _length(x) -> int:
@@ -111,7 +126,7 @@ class MultiLevelMODWTResult:
         return _energy(self._app)
 
     def getTotalEnergy(self) -> float:
-        return self.getApproximationEnergy() + sum(self.getDetailEnergyAtLevel(j) for j in range(1, self.getLevels() + 1))
+        return _total_energy(self)
 
     def getRelativeEnergyDistribution(self) -> List[float]:
         # immutable impl order: [approx, d1..dJ]  (core/modwt/MultiLevelMODWTResultImpl.java:121-138)
