@@ -108,10 +108,14 @@ def parse(argv=None):
                    help="HIP events around every kernel launch inside the timed steps (inline) or none")
     p.add_argument("--contexts", type=int, default=0,
                    help="contexts (each on its own stream) sharing a GPU's rows; 0 = policy (see run())")
-    p.add_argument("--rotate", type=int, default=1,
-                   help="R buffer sets, step i reading set i mod R (R * input bytes beyond the 256 MiB Infinity "
-                        "Cache: no step re-reads what an earlier one left on die); 1 = one set")
-    p.add_argument("--rotate-outputs", action="store_true", help="--rotate also the output buffers")
+    p.add_argument("--rotate", type=int, default=0,
+                   help="R buffer sets, step i working on set i mod R, so no step re-reads an input an earlier step "
+                        "left in the 256 MiB Infinity Cache; 0 = auto (R * input bytes >= 512 MiB, R >= 2, "
+                        "outputs rotated too); 1 = one set (the round-1..3 method)")
+    p.add_argument("--rotate-outputs", action="store_true", help="explicit --rotate R: rotate the outputs too")
+    p.add_argument("--overlap-steps", action="store_true",
+                   help="experiment: pipeline step i+1's forward with step i's inverse on two contexts "
+                        "(needs --rotate >= 2 --rotate-outputs; prints one line, no kernel roofline)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--dry-run", action="store_true",
@@ -393,6 +397,74 @@ class Part:
         return step
 
 
+def measure_overlap(torch, dist, world, pt, eng_i, stream_i, flags, steps, warmup, settle_s):
+    """Experiment (`--overlap-steps`): consecutive steps pipelined over two contexts on two streams --
+    every forward on the part's context / stream F, every inverse on context I / stream I, step i's
+    inverse after its forward (event), step i's forward after step i - R's inverse (the buffer set it
+    overwrites), R >= 2 rotated output sets.  So step i + 1's forward overlaps step i's inverse; each
+    step still runs its full forward and inverse.  Direct C-ABI calls (no graph).  Returns device seconds
+    of the K timed steps (events on stream F around them, stream I joined back)."""
+    nat, lib, w, J, N, B = pt.nat, pt.lib, pt.w, pt.J, pt.N, pt.rows
+    R = pt.rotate
+    assert R >= 2 and pt.pipeline == "fwd+inv", "--overlap-steps needs --rotate >= 2 --rotate-outputs, fwd+inv"
+    p = lambda t: c_void_p(t.data_ptr())  # noqa: E731
+    fwd = lib.vw_modwt_forward_f32 if pt.f32 else lib.vw_modwt_forward_f64
+    inv = lib.vw_modwt_inverse_f32 if pt.f32 else lib.vw_modwt_inverse_f64
+    ptrs = [(p(st["x"]), p(st["det"]), p(st["app"]), p(st["y"])) for st in pt.sets]
+    sF, sI = pt.stream, stream_i
+    eF, eI = pt.eng, eng_i
+    with torch.cuda.stream(sI):
+        eI.bind_torch_stream()
+    with torch.cuda.stream(sF):
+        eF.bind_torch_stream()
+    ev_inv = {}
+
+    def one(i):
+        r = i % R
+        xp, dp, ap, yp = ptrs[r]
+        if i - R in ev_inv:
+            sF.wait_event(ev_inv.pop(i - R))
+        pt._check(fwd(eF.ctx, xp, B, N, N, pt.lo_a, pt.hi_a, pt.L, w.wavelet_id, nat.PERIODIC, J, flags, dp, ap))
+        ef = torch.cuda.Event()
+        ef.record(sF)
+        sI.wait_event(ef)
+        pt._check(inv(eI.ctx, dp, ap, B, N, pt.lo_a, pt.hi_a, pt.L, w.wavelet_id, nat.PERIODIC, J, 0xFFFFFFFF, 0,
+                      flags, yp))
+        ei = torch.cuda.Event()
+        ei.record(sI)
+        ev_inv[i] = ei
+        pt.last = r
+
+    def join():
+        e = torch.cuda.Event()
+        e.record(sI)
+        sF.wait_event(e)
+        ev_inv.clear()
+
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < settle_s or n < warmup:
+        one(n)
+        n += 1
+        if n % 20 == 0:
+            torch.cuda.synchronize()
+    join()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(sF)
+    for i in range(steps):
+        one(n + i)
+    join()
+    ev1.record(sF)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    return ev0.elapsed_time(ev1) * 1e-3
+
+
 class Workload:
     """A rank's rows split over K contexts of its GPU (contiguous blocks, shard_rows), each on its own
     stream: with K = 2 one part's inverse overlaps the other's forward tail (and the two parts' first
@@ -624,7 +696,28 @@ def run(args, world, rank, local):
     K = args.contexts or (2 if rows >= 1024 else 1)
     engines = [vw.Engine.get(local)] + [vw.Engine(local) for _ in range(K - 1)]
     streams = [main] + [torch.cuda.Stream(device=dev) for _ in range(K - 1)]
-    rot = (args.rotate, args.rotate_outputs)
+    # Buffer sets: with one set the same 128 MiB input was re-read every step and stayed in
+    # the Infinity Cache (the persistent forward's LDS-DMA allocates there, the streaming loads and stores
+    # around it are non-temporal): same box, db4 4096 x 4096, forward 0.163-0.164 ms with one set vs
+    # 0.187-0.197 ms with three (profiles/r04/ab_rotate_4096.log).  So every step reads a fresh input.
+    x_bytes = rows * N * esz
+    R = args.rotate or max(2, -(-(512 << 20) // max(x_bytes, 1)))
+    rot = (R, bool(args.rotate_outputs or not args.rotate))
+    if args.overlap_steps:
+        wl = Workload(engines[:1], streams[:1], w, J, rows, N, dtype, pipeline, start, torch, *rot)
+        ei = vw.Engine(local)
+        si = torch.cuda.Stream(device=dev)
+        el = measure_overlap(torch, dist, world, wl.parts[0], ei, si, flags, args.steps, args.warmup, args.settle)
+        el = max_over_ranks(torch, dist, world, el, dev)
+        check = verify(torch, wl, w, J, pipeline, flags, nat)
+        if rank == 0:
+            print(json.dumps({"experiment": "overlap-steps", "value": round(Bg * N * args.steps / el / 1e6, 2),
+                              "unit": "Msamples/s", "n_gpus": world, "ms_per_step": round(el / args.steps * 1e3, 4),
+                              "batch_per_gpu": rows, "buffer_sets": args.rotate, "check": check}), flush=True)
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     wl = Workload(engines, streams, w, J, rows, N, dtype, pipeline, start, torch, *rot)
     footprint = sum(pt.footprint() for pt in wl.parts)
     (elapsed, host_elapsed), (settle_s, settle_steps), fams, sampled, pass_ms = measure(
@@ -760,8 +853,9 @@ def run(args, world, rank, local):
                                + (f", {K} contexts per GPU (own stream each, row blocks)" if K > 1 else ""),
                 "contexts_per_gpu": K,
                 "launch": LAUNCH_DESC[args.launch],
-                "buffer_sets": {"sets": args.rotate, "outputs_rotated": bool(args.rotate_outputs),
-                                "device_bytes_per_rank": footprint},
+                "buffer_sets": {"sets": rot[0], "outputs_rotated": rot[1], "device_bytes_per_rank": footprint,
+                                "why": "step i works on set i mod R: no step re-reads an input an earlier step left "
+                                       "in the 256 MiB Infinity Cache"},
                 "passes_ms": {f: round(v, 5) for f, v in kpass_ms.items()},
                 "kernel_timing": (f"HIP events around every kernel launch of {sampled} of the {args.steps} timed "
                                   "steps (event nodes inside the replayed graph)" if args.launch == "graph-k" else

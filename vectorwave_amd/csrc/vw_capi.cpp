@@ -72,6 +72,7 @@ struct Tuning {
   bool force_tiled = false;// VW_FORCE_TILED: per-level path even when the fused kernels fit
   int fwd_rev = 0, inv_rev = 0;  // VW_FWD_REV / VW_INV_REV: reverse workgroup -> signal walk
   int inv_persist = 0;           // VW_INV_PERSIST=1: persistent two-region inverse (k_inverse_persist)
+  int dma_nt = 0;                // VW_DMA_NT=1: non-temporal LDS-DMA of signal rows (persistent kernels)
   int fwd_tile = 0;        // VW_FWD_TILE: per-level forward tile (0 = default)
   bool multi = true;       // VW_MULTI=0: one launch per level on the long-signal path
   int multi_div = 4;       // VW_MULTI_DIV: reach bound of a level group = tile / div
@@ -118,6 +119,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_FWD_REV") t.fwd_rev = v < 0 ? 0 : v;
   else if (k == "VW_INV_REV") t.inv_rev = v < 0 ? 0 : v;
   else if (k == "VW_INV_PERSIST") t.inv_persist = v < 0 ? d.inv_persist : v;
+  else if (k == "VW_DMA_NT") t.dma_nt = v < 0 ? d.dma_nt : v;
   else if (k == "VW_FWD_TILE") t.fwd_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI") t.multi = v < 0 ? d.multi : v != 0;
   else if (k == "VW_MULTI_DIV") t.multi_div = v <= 0 ? d.multi_div : v;
@@ -157,7 +159,7 @@ static const char* const kTuningKeys[] = {
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
     "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8",
-    "VW_INV_PERSIST", "VW_MULTI_XCD"};
+    "VW_INV_PERSIST", "VW_MULTI_XCD", "VW_DMA_NT"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -1021,6 +1023,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     a.unrolled = a.vec_io && fit && L <= tu.unroll_max;
     a.validate = validate; a.bad = c->bad;
     a.rev = tu.fwd_rev;
+    a.dma_nt = tu.dma_nt;
     for (int j = 0; j < J; ++j) a.hist[j] = hist ? hist[j] : nullptr;
     a.hist_update = hist_update ? 1 : 0;
     a.taps = L;
@@ -1304,6 +1307,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     a.hlpad_a = hlpad; a.hlpad_d = hlpad; a.region_d = (int)region;
     if (persist) {
       a.persist = 1;
+      a.dma_nt = tu.dma_nt;
       a.dma_vec = (int)dma_vec;
       a.region_d = (int)(dma_vec * V);
     }

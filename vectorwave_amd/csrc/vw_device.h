@@ -793,14 +793,24 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_fused(const FwdA
 // approximation rows) follow the DMA, so vmcnt(2*NV) retires the DMA and leaves those stores in
 // flight.  Host contract (vw_capi.cpp): two buffers, every slab full (threads*NV == N/V), whole
 // waves, N/V a multiple of 64 (one wave instruction = 64 x 16 B), no validation, no history.
-template <typename T>
-__device__ __forceinline__ void dma_row(T* buf, const T* __restrict__ src, int nvec) {
-  constexpr int V = VT<T>::V;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  for (int c = wv; c * 64 < nvec; c += nw) {
-    const T* g = src + (size_t)(c * 64 + lane) * V;
-    const unsigned lds = (unsigned)(uintptr_t)(buf + c * 64 * V);  // LDS byte address (wave-uniform)
-    unsigned keep;
+// One wave instruction of LDS-DMA: 64 lanes x 16 bytes from per-lane global addresses into 1 KiB of
+// LDS at the wave-uniform byte address `lds` (global_load_lds_dwordx4; no VGPR is written).  nt: the
+// non-temporal cache policy (a row read once by this launch need not be kept in L2 / Infinity Cache).
+// Issued from inline asm so the compiler's waitcnt pass does not wait for it before unrelated LDS
+// reads; the caller retires it with an explicit vmcnt wait.
+__device__ __forceinline__ void lds_dma16(unsigned lds, const void* g, bool nt) {
+  unsigned keep;
+  if (nt) {
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off nt\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
+        : "memory");
+  } else {
     asm volatile(
         "s_mov_b32 %0, m0\n\t"
         "s_mov_b32 m0, %2\n\t"
@@ -813,6 +823,14 @@ __device__ __forceinline__ void dma_row(T* buf, const T* __restrict__ src, int n
   }
 }
 
+template <typename T>
+__device__ __forceinline__ void dma_row(T* buf, const T* __restrict__ src, int nvec, bool nt) {
+  constexpr int V = VT<T>::V;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
+  for (int c = wv; c * 64 < nvec; c += nw)
+    lds_dma16((unsigned)(uintptr_t)(buf + c * 64 * V), src + (size_t)(c * 64 + lane) * V, nt);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -821,7 +839,8 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 // vmcnt(n) for a wave-uniform runtime n (0..63; larger waits for 63, i.e. for more)
 __device__ __forceinline__ void wait_vmcnt_rt(int n) {
-  switch (n) {
+  // the count is wave-uniform; without this the switch compiles to an exec-masked compare tree on a VGPR
+  switch (__builtin_amdgcn_readfirstlane(n)) {
     case 0: wait_vmcnt<0>(); break;
     case 1: wait_vmcnt<1>(); break;
     case 2: wait_vmcnt<2>(); break;
@@ -903,7 +922,7 @@ k_forward_persist(const FwdArgs<T> p) {
   long long b = blockIdx.x;
   if (b >= p.B) return;
   int cur = 0;
-  dma_row<T>(B0, p.x + b * p.ldx, nvec);
+  dma_row<T>(B0, p.x + b * p.ldx, nvec, p.dma_nt != 0);
   wait_vmem();
   for (;;) {
     T* X = cur ? B1 : B0;
@@ -916,7 +935,7 @@ k_forward_persist(const FwdArgs<T> p) {
     for (int j = 1; j <= p.J; ++j) {
       const LevelDesc lv = p.lv[j - 1];
       lds_barrier();  // X = level input + halo; every read of Y (previous level) done
-      if (j == p.J && bn < p.B) dma_row<T>(Y, p.x + bn * p.ldx, nvec);  // next signal -> free buffer
+      if (j == p.J && bn < p.B) dma_row<T>(Y, p.x + bn * p.ldx, nvec, p.dma_nt != 0);  // next signal -> free buffer
       T* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
       T* aout = (j == p.J) ? p.approx + b * (size_t)N : nullptr;
       fwd_level<T, L, FMA, NV, false>(p, X, nvec, lv, dout, aout, true, 0ull, areg);
@@ -1115,30 +1134,19 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, VW_INV_W)) k_inverse_seq(const
 // vectors re-read the row's first vectors, v - N/V).
 // DMA wave-instructions this wave issues for a row of tvec vectors (dma_row_periodic's loop count)
 __device__ __forceinline__ int dma_count(int tvec) {
-  const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6, nc = tvec / 64;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6, nc = tvec / 64;
   return wv < nc ? (nc - wv + nw - 1) / nw : 0;
 }
 
 template <typename T>
-__device__ __forceinline__ int dma_row_periodic(T* buf, const T* __restrict__ src, int nvec, int tvec) {
+__device__ __forceinline__ int dma_row_periodic(T* buf, const T* __restrict__ src, int nvec, int tvec, bool nt) {
   constexpr int V = VT<T>::V;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
   int n = 0;
-  for (int c = wv; c * 64 < tvec; c += nw, ++n) {
+  for (int c = wv; c * 64 < tvec; c += nw, ++n) {  // wave-uniform loop (scalar wv)
     int v = c * 64 + lane;
     v = v < nvec ? v : v - nvec;
-    const T* g = src + (size_t)v * V;
-    const unsigned lds = (unsigned)(uintptr_t)(buf + c * 64 * V);  // LDS byte address (wave-uniform)
-    unsigned keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(g), "s"(__builtin_amdgcn_readfirstlane(lds))
-        : "memory");
+    lds_dma16((unsigned)(uintptr_t)(buf + c * 64 * V), src + (size_t)v * V, nt);
   }
   return n;
 }
@@ -1159,8 +1167,8 @@ k_inverse_persist(const InvArgs<T> p) {
   const size_t plane = (size_t)p.B * (size_t)N;
   long long b = blockIdx.x;
   if (b >= p.B) return;
-  dma_row_periodic<T>(Q, p.approx + b * (size_t)N, nvec, tvec);
-  dma_row_periodic<T>(P, p.details + (size_t)(J - 1) * plane + b * (size_t)N, nvec, tvec);
+  dma_row_periodic<T>(Q, p.approx + b * (size_t)N, nvec, tvec, p.dma_nt != 0);
+  dma_row_periodic<T>(P, p.details + (size_t)(J - 1) * plane + b * (size_t)N, nvec, tvec, p.dma_nt != 0);
   wait_vmcnt_rt(dma_count(tvec));  // a_J landed (d_J may still be in flight)
   for (;;) {
     const long long bn = b + G;
@@ -1172,18 +1180,18 @@ k_inverse_persist(const InvArgs<T> p) {
       inv_row<T, L, FMA, NV>(Q, nvec, lv.s, lv.dir_a, lv.off_a, p.lo, p.taps, acc);
       wait_vmem();    // this wave's share of d_j (the only vector-memory operations in flight but stores)
       lds_barrier();  // P = d_j + halo; every read of Q done
-      if (j == 1 && bn < p.B) dma_row_periodic<T>(Q, p.approx + bn * (size_t)N, nvec, tvec);  // next a_J
+      if (j == 1 && bn < p.B) dma_row_periodic<T>(Q, p.approx + bn * (size_t)N, nvec, tvec, p.dma_nt != 0);  // next a_J
       inv_row<T, L, FMA, NV>(P, nvec, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
       if (j > 1) {
         lds_barrier();  // every read of P done
-        dma_row_periodic<T>(P, p.details + (size_t)(j - 2) * plane + b * (size_t)N, nvec, tvec);
+        dma_row_periodic<T>(P, p.details + (size_t)(j - 2) * plane + b * (size_t)N, nvec, tvec, p.dma_nt != 0);
         regs_to_level<T, L, NV>(Q, acc, nvec, N, p.lv[j - 2], 0, (const T*)nullptr);
       }
     }
     for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, w * V, N, true, acc[k]); });
     if (bn >= p.B) break;
     lds_barrier();  // every read of P (level 1's detail branch) done
-    const int nd = dma_row_periodic<T>(P, p.details + (size_t)(J - 1) * plane + bn * (size_t)N, nvec, tvec);
+    const int nd = dma_row_periodic<T>(P, p.details + (size_t)(J - 1) * plane + bn * (size_t)N, nvec, tvec, p.dma_nt != 0);
     wait_vmcnt_rt(NV + nd);  // the next a_J landed; the y stores and the d_J DMA stay in flight
     b = bn;
   }

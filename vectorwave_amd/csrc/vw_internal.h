@@ -54,7 +54,8 @@ struct FwdArgs {
   int hlpad;            // LDS offset of element 0 (multiple of the vector width)
   int region1;          // element offset of the second level buffer (0 = single buffer)
   int vec_io;
-  int unrolled;         // 1: the tap-unrolled kernel may run (aligned rows, full slabs; vw_capi fused_plan)           // 1: rows and outputs are 16-B aligned -> vector global I/O
+  int unrolled;         // 1: the tap-unrolled kernel may run (aligned rows, full slabs; vw_capi fused_plan)
+  int dma_nt;           // k_forward_persist: non-temporal LDS-DMA of the signal rows
   int validate;         // 1: non-finite check on input and outputs (atomicMin into *bad)
   int rev;              // 1: workgroup g owns signal B-1-g (walk order, see vw_capi.cpp walk_reverse)
   unsigned long long* bad;
@@ -93,6 +94,7 @@ struct InvArgs {
   int tap_lds;          // k_inverse_blk: element offset of the LDS tap table
   int blk_tight;        // k_inverse_blk: sparse padding (blk_layout)
   int persist;          // 1: k_inverse_persist (two regions, LDS-DMA rows, resident grid walks the batch)
+  int dma_nt;           // k_inverse_persist: non-temporal LDS-DMA of the rows
   int dma_vec;          // k_inverse_persist: vectors per DMA'd row incl. the periodic right halo (x64)
   T lo[kMaxTaps];
   T hi[kMaxTaps];
