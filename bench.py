@@ -397,13 +397,14 @@ class Part:
         return step
 
 
-def measure_overlap(torch, dist, world, pt, eng_i, stream_i, flags, steps, warmup, settle_s):
+def measure_overlap(torch, dist, world, pt, eng_i, stream_i, flags, steps, warmup, settle_s, use_graph=True):
     """Experiment (`--overlap-steps`): consecutive steps pipelined over two contexts on two streams --
     every forward on the part's context / stream F, every inverse on context I / stream I, step i's
     inverse after its forward (event), step i's forward after step i - R's inverse (the buffer set it
     overwrites), R >= 2 rotated output sets.  So step i + 1's forward overlaps step i's inverse; each
-    step still runs its full forward and inverse.  Direct C-ABI calls (no graph).  Returns device seconds
-    of the K timed steps (events on stream F around them, stream I joined back)."""
+    step still runs its full forward and inverse.  The K timed steps are recorded into one graph (or
+    issued as direct C-ABI calls, use_graph=False).  Returns device seconds of the K timed steps (events
+    on stream F around them, stream I joined back)."""
     nat, lib, w, J, N, B = pt.nat, pt.lib, pt.w, pt.J, pt.N, pt.rows
     R = pt.rotate
     assert R >= 2 and pt.pipeline == "fwd+inv", "--overlap-steps needs --rotate >= 2 --rotate-outputs, fwd+inv"
@@ -450,14 +451,28 @@ def measure_overlap(torch, dist, world, pt, eng_i, stream_i, flags, steps, warmu
             torch.cuda.synchronize()
     join()
     torch.cuda.synchronize()
+    graph = None
+    if use_graph:
+        # the K timed steps (both streams, their event edges) recorded once into one graph (torch stream
+        # capture from stream F; stream I joins through the events and rejoins before the end)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=sF):
+            for i in range(steps):
+                one(n + i)
+            join()
+        graph.replay()   # first replay (upload) outside the timed region
+        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(sF)
-    for i in range(steps):
-        one(n + i)
-    join()
+    if graph is not None:
+        graph.replay()
+    else:
+        for i in range(steps):
+            one(n + i)
+        join()
     ev1.record(sF)
     torch.cuda.synchronize()
     if world > 1:
@@ -707,7 +722,8 @@ def run(args, world, rank, local):
         wl = Workload(engines[:1], streams[:1], w, J, rows, N, dtype, pipeline, start, torch, *rot)
         ei = vw.Engine(local)
         si = torch.cuda.Stream(device=dev)
-        el = measure_overlap(torch, dist, world, wl.parts[0], ei, si, flags, args.steps, args.warmup, args.settle)
+        el = measure_overlap(torch, dist, world, wl.parts[0], ei, si, flags, args.steps, args.warmup, args.settle,
+                             args.launch != "direct")
         el = max_over_ranks(torch, dist, world, el, dev)
         check = verify(torch, wl, w, J, pipeline, flags, nat)
         if rank == 0:

@@ -73,6 +73,7 @@ struct Tuning {
   int fwd_rev = 0, inv_rev = 0;  // VW_FWD_REV / VW_INV_REV: reverse workgroup -> signal walk
   int inv_persist = 0;           // VW_INV_PERSIST=1: persistent two-region inverse (k_inverse_persist)
   int dma_nt = 0;                // VW_DMA_NT=1: non-temporal LDS-DMA of signal rows (persistent kernels)
+  int fwd_stream = 0;            // VW_FWD_STREAM=1: streaming multi-level forward for long PERIODIC signals
   int fwd_tile = 0;        // VW_FWD_TILE: per-level forward tile (0 = default)
   bool multi = true;       // VW_MULTI=0: one launch per level on the long-signal path
   int multi_div = 4;       // VW_MULTI_DIV: reach bound of a level group = tile / div
@@ -120,6 +121,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_INV_REV") t.inv_rev = v < 0 ? 0 : v;
   else if (k == "VW_INV_PERSIST") t.inv_persist = v < 0 ? d.inv_persist : v;
   else if (k == "VW_DMA_NT") t.dma_nt = v < 0 ? d.dma_nt : v;
+  else if (k == "VW_FWD_STREAM") t.fwd_stream = v < 0 ? d.fwd_stream : v;
   else if (k == "VW_FWD_TILE") t.fwd_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI") t.multi = v < 0 ? d.multi : v != 0;
   else if (k == "VW_MULTI_DIV") t.multi_div = v <= 0 ? d.multi_div : v;
@@ -159,7 +161,7 @@ static const char* const kTuningKeys[] = {
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
     "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8",
-    "VW_INV_PERSIST", "VW_MULTI_XCD", "VW_DMA_NT"};
+    "VW_INV_PERSIST", "VW_MULTI_XCD", "VW_DMA_NT", "VW_FWD_STREAM"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -816,6 +818,43 @@ static void set_halo_images(LevelDesc& d, int64_t N, int64_t npow2, int V, int t
   d.own = (d.hl <= N && d.hr <= N && d.vs <= threads && (int64_t)d.ve >= (int64_t)(nv - 1) * threads) ? 1 : 0;
 }
 
+// Streaming forward plan (vw_device.h k_forward_stream) from level j: the most consecutive PERIODIC
+// levels whose LDS rings (history (L-1)*s + one chunk of 1024 vectors each; ring 0 a multiple of 64
+// vectors for the DMA) fit one workgroup's LDS; segments so that B * seg fills the CUs.  Returns the
+// group size (0: not applicable).
+template <typename T>
+static int stream_plan(const std::vector<LevelDesc>& lv, int j, int J, int L, int64_t N, int64_t B, int cus,
+                       StreamArgs<T>* a) {
+  constexpr int V = vec_width<T>();
+  constexpr int64_t C = (int64_t)kStreamThreads * V;
+  if (N % C != 0 || N < 8 * C) return 0;
+  const int64_t budget = kLdsBytes / (int64_t)sizeof(T);
+  int g = 0;
+  int64_t used = 0, hist = 0;
+  int cap[kMaxGroup];
+  while (j + g <= J && g < kMaxGroup && lv[j + g - 1].mode == kHaloPeriodic) {
+    const int64_t h = (int64_t)(L - 1) * lv[j + g - 1].s;
+    const int64_t cp = g == 0 ? round_up(h + C, 64 * V) : round_up(h + C, V);
+    if (used + cp > budget) break;
+    cap[g] = (int)cp;
+    used += cp;
+    hist += h;
+    ++g;
+  }
+  if (g < 2) return 0;
+  const int64_t warm = round_up(hist, C);
+  if (warm > N) return 0;
+  int seg = 1;
+  while (B * seg < cus && N / (2 * seg) >= 4 * C && (N / (2 * seg)) % C == 0) seg *= 2;
+  if (a) {
+    a->g = g; a->N = (int)N; a->B = B; a->s0 = lv[j - 1].s;
+    a->seg = seg; a->seglen = (int)(N / seg); a->warm = (int)warm;
+    int64_t off = 0;
+    for (int k = 0; k < g; ++k) { a->cap[k] = cap[k]; a->off[k] = (int)off; off += cap[k]; }
+  }
+  return g;
+}
+
 // Level groups of the per-level path (vw_device.h k_forward_multi / k_inverse_multi): from level 1
 // up, consecutive PERIODIC levels run as one multi-level tile launch while their combined reach
 // sum((L-1)*s_j) stays within a quarter of the tile (the redundant arithmetic).  groups[j-1] = size
@@ -1097,6 +1136,33 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     const std::vector<int> groups = level_groups(tu, lv, J, L, V, mtile, !validate && !hist);
     for (int j = 1; j <= J; ++j) {
       T* const nxt = (src == tmp[0]) ? tmp[1] : tmp[0];  // never the level's own input
+      // streaming multi-level forward from level j (VW_FWD_STREAM)
+      if (tu.fwd_stream && !validate && !hist && (lda % V) == 0 && aligned16(src) && aligned16(details) &&
+          aligned16(approx) && has_unrolled_taps(L) && L <= tu.unroll_max) {
+        StreamArgs<T> sa;
+        memset(&sa, 0, sizeof(sa));
+        const int g = stream_plan<T>(lv, j, J, L, N, B, c->cus, &sa);
+        if (g >= 2) {
+          const int je = j + g - 1;
+          sa.src = src; sa.lda = lda; sa.taps = L; sa.dma_nt = tu.dma_nt;
+          sa.out = (je == J) ? approx : nxt;
+          for (int k = 0; k < g; ++k) sa.out_d[k] = details + (size_t)(j - 1 + k) * plane;
+          copy_taps(sa.lo, lo, L);
+          copy_taps(sa.hi, hi, L);
+          int lds = 0;
+          for (int k = 0; k < g; ++k) lds += sa.cap[k];
+          lds *= (int)sizeof(T);
+          {
+            LaunchTimer lt(c, "forward_level");
+            hipError_t e = launch_forward_stream<T>(sa, lds, fma, c->stream);
+            if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward stream launch failed: %s", hipGetErrorString(e));
+          }
+          src = sa.out;
+          lda = N;
+          j = je;
+          continue;
+        }
+      }
       // streaming deep group from level j: the longest run j..je within the LDS budget
       if (groups[j - 1] == 1 && !validate && !hist && (lda % V) == 0 && aligned16(src) && aligned16(details) &&
           aligned16(approx) && deep_plan<T>(tu, lv, j, j, L, N, false, nullptr)) {

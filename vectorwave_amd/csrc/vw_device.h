@@ -2220,6 +2220,150 @@ __global__ void __launch_bounds__(12 * R) k_inverse_sweep3(const LevelArgs<T> p)
 }
 
 // ---------------------------------------------------------------------------------------------
+// Streaming multi-level forward for long PERIODIC signals (BatchStreamingMODWT's 2^20-sample blocks:
+// BatchStreamingMODWT.java:110-158 -> BatchSIMDMODWT.batchMultiLevelMODWTSoA :343-424; the cascade of
+// MultiLevelMODWTTransform.decompose :243-251 with ScalarOps.circularConvolveMODWT :700-723 per level).
+//
+// One workgroup streams one segment of one signal, left to right, in chunks of C = 1024 vectors.  Level
+// k of the group keeps its INPUT in an LDS ring: the last H_k = (L-1)*s_k samples (what the next chunk
+// still reads) plus the chunk being produced.  Per chunk every level runs once -- read its ring, write
+// d_k to HBM and its approximation into ring k+1 (the last level's to HBM) -- so x is read once, each
+// output written once, nothing is recomputed (the multi-level tiles re-read and re-compute their reach,
+// the per-level sweeps round-trip every approximation through HBM).  The input chunk c+1 arrives by
+// LDS-DMA into ring 0 while levels 2..g of chunk c compute.
+//
+// Periodic boundary: the stream starts `warm` samples before the segment (positions mod N).  Level k's
+// outputs depend on its inputs back to sum_{m<=k} H_m samples; from stream position warm >= sum H on,
+// every ring holds exactly the values the reference's (t - l) mod N would read, so the stored outputs
+// are the reference's (the warm-up ones, computed from not-yet-valid ring slots, are never stored).
+// Per output both filters from one read per tap, taps ascending: bit-exact in EXACT mode.
+//
+// Thread t owns vector t of every chunk (samples u = t*V .. t*V+V-1).  A ring slot is the stream
+// position mod the ring's capacity; a chunk's base slot per ring is workgroup-uniform, each read wraps
+// with two selects (the history reaches back up to H_k, the chunk forward up to C).
+template <typename T>
+__device__ __forceinline__ int ring_slot(int sl, int cap) {
+  sl += sl < 0 ? cap : 0;
+  return sl - (sl >= cap ? cap : 0);
+}
+
+template <typename T, int L, bool FMA, int S>
+__device__ __forceinline__ void stream_window(const T* ring, int cap, int base, const T* lo, const T* hi,
+                                              T (&al)[VT<T>::V], T (&ah)[VT<T>::V]) {
+  // S = 1 / 2: a register window of aligned vectors (fwd_window's chunks), each vector's slot wrapped
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  static_for<0, (L + kWinTaps - 1) / kWinTaps>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * kWinTaps;
+    constexpr int I1 = (I0 + kWinTaps < L) ? I0 + kWinTaps : L;
+    constexpr int A = floor_div(-(I1 - 1) * S, V) * V;
+    constexpr int E = (floor_div(V - 1 - I0 * S, V) + 1) * V;
+    constexpr int NE = E - A;
+    T w[NE];
+#pragma unroll
+    for (int k = 0; k < NE / V; ++k) {
+      const vec v = *reinterpret_cast<const vec*>(ring + ring_slot<T>(base + A + k * V, cap));
+#pragma unroll
+      for (int e = 0; e < V; ++e) w[k * V + e] = v[e];
+    }
+#pragma unroll
+    for (int i = I0; i < I1; ++i) {
+      vmadd<FMA, kPkFwd>(al, &w[-i * S - A], lo[i]);
+      vmadd<FMA, kPkFwd>(ah, &w[-i * S - A], hi[i]);
+    }
+  });
+}
+
+template <typename T, int L, bool FMA>
+__device__ __forceinline__ void stream_level(const T* ring, int cap, int base, int s, const T* lo, const T* hi,
+                                             T (&al)[VT<T>::V], T (&ah)[VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+#pragma unroll
+  for (int e = 0; e < V; ++e) { al[e] = T(0); ah[e] = T(0); }
+  if (s == 1) return stream_window<T, L, FMA, 1>(ring, cap, base, lo, hi, al, ah);
+  if constexpr (V == 4) {
+    if (s == 2) return stream_window<T, L, FMA, 2>(ring, cap, base, lo, hi, al, ah);
+  }
+#pragma unroll
+  for (int i = 0; i < L; ++i) {  // s a multiple of V: aligned 16-byte reads
+    const vec v = *reinterpret_cast<const vec*>(ring + ring_slot<T>(base - i * s, cap));
+    vmadd<FMA, kPkFwd>(al, v, lo[i]);
+    vmadd<FMA, kPkFwd>(ah, v, hi[i]);
+    if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // <= 4 reads in flight
+  }
+}
+
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(kStreamThreads) k_forward_stream(const StreamArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  constexpr int C = kStreamThreads * V;  // samples per chunk
+  using vec = typename VT<T>::v;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* const lds = reinterpret_cast<T*>(smem);
+  const long long b = blockIdx.x / p.seg;
+  const int sg = blockIdx.x % p.seg;
+  if (b >= p.B) return;
+  const int N = p.N;
+  const int u = threadIdx.x * V;                     // this thread's samples within a chunk
+  const int q0 = sg * p.seglen;                      // first stored output of the segment
+  const int nc = (p.warm + p.seglen) / C;            // chunks streamed
+  const int wc = p.warm / C;                         // warm-up chunks (nothing stored)
+  int pos0 = q0 - p.warm;                            // signal position of stream position 0
+  while (pos0 < 0) pos0 += N;
+  const T* __restrict__ src = p.src + b * p.lda;
+  const size_t row = (size_t)b * (size_t)N;
+  const bool nt = p.dma_nt != 0;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  auto wrapN = [&](int q) { q -= q >= N ? N : 0; return q - (q >= N ? N : 0); };  // q < 3N
+  // chunk c of the input -> ring 0 (one 64-vector DMA instruction per wave: 16 waves x 1 KiB)
+  auto dma_chunk = [&](int c, int cbase) {  // cbase: ring-0 slot of the chunk (a multiple of 64 vectors)
+    int sl = cbase + wv * 64 * V;
+    sl -= sl >= p.cap[0] ? p.cap[0] : 0;
+    const int q = wrapN(pos0 + c * C + (wv * 64 + lane) * V);
+    lds_dma16((unsigned)(uintptr_t)(lds + p.off[0] + sl), src + q, nt);
+  };
+  int base[kMaxGroup];                               // chunk base slot per ring (uniform)
+#pragma unroll
+  for (int k = 0; k < kMaxGroup; ++k) base[k] = 0;
+  dma_chunk(0, 0);
+  wait_vmem();
+  for (int c = 0; c < nc; ++c) {
+    const bool store = c >= wc;
+    const int q = wrapN(pos0 + c * C + u);           // signal position of this thread's first sample
+    for (int k = 0; k < p.g; ++k) {
+      lds_barrier();  // ring k holds the level's input up to this chunk; every read of its slots being
+                      // overwritten below is done
+      if (k == 1 && c + 1 < nc) {                    // ring 0's chunk-c reads are done (level 0 finished)
+        const int nb = base[0] + C;
+        dma_chunk(c + 1, nb - (nb >= p.cap[0] ? p.cap[0] : 0));
+      }
+      const int s = p.s0 << k;
+      T al[V], ah[V];
+      stream_level<T, L, FMA>(lds + p.off[k], p.cap[k], base[k] + u, s, p.lo, p.hi, al, ah);
+      vec oa, od;
+#pragma unroll
+      for (int e = 0; e < V; ++e) { oa[e] = al[e]; od[e] = ah[e]; }
+      if (store) {
+        stream_store<VW_FWD_STORE_AUX, vec>(p.out_d[k] + row, q / V, od);
+        if (k == p.g - 1) stream_store<VW_FWD_STORE_AUX, vec>(p.out + row, q / V, oa);
+      }
+      if (k + 1 < p.g) *reinterpret_cast<vec*>(lds + p.off[k + 1] + ring_slot<T>(base[k + 1] + u, p.cap[k + 1])) = oa;
+    }
+    // the next chunk's base slot in every ring
+#pragma unroll
+    for (int k = 0; k < kMaxGroup; ++k) {
+      if (k < p.g) {
+        int nb = base[k] + C;
+        base[k] = nb - (nb >= p.cap[k] ? p.cap[k] : 0);
+      }
+    }
+    if (c + 1 < nc) wait_vmcnt_rt(store ? p.g : 0);  // this wave's DMA of chunk c+1; the stores stay in flight
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Multi-level tiles for long PERIODIC signals (host: vw_capi.cpp level_groups).  One workgroup runs
 // a group of consecutive levels over one tile of one signal; the intermediate approximations stay
 // in LDS.  Periodic convolution commutes with shifts, so a level evaluated at a position v outside

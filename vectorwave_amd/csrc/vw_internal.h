@@ -168,6 +168,30 @@ struct MultiArgs {
   T hi[kMaxTaps];
 };
 
+// Streaming multi-level forward (PERIODIC, long signals; vw_device.h k_forward_stream): levels j0 ..
+// j0+g-1 of one signal segment in one launch, each level's input kept in an LDS ring (its history of
+// (L-1)*s samples plus one chunk), the input streamed in chunks of 1024 vectors by LDS-DMA.
+constexpr int kStreamThreads = 1024;
+template <typename T>
+struct StreamArgs {
+  const T* src;              // input of level j0 [B][lda]
+  long long lda;
+  T* out_d[kMaxGroup];       // d of level j0+k [B][N]
+  T* out;                    // approximation of level j0+g-1 [B][N]
+  long long B;
+  int N;
+  int g;                     // levels
+  int s0;                    // spacing of level j0
+  int seg, seglen;           // segments per signal, stored outputs per segment (multiple of the chunk)
+  int warm;                  // warm-up samples streamed before each segment (multiple of the chunk)
+  int cap[kMaxGroup];        // ring capacities (elements; ring 0 a multiple of 64 vectors)
+  int off[kMaxGroup];        // ring offsets (elements)
+  int dma_nt;
+  int taps;
+  T lo[kMaxTaps];
+  T hi[kMaxTaps];
+};
+
 // WaveletDenoiser threshold methods (core/denoising/WaveletDenoiser.java:588-622) and the per-launch
 // constants of the threshold kernels (vw_sigma.h).
 enum ThrMethod { kThrUniversal = 0, kThrSure = 1, kThrMinimax = 2, kThrBayes = 3, kThrFixed = 4 };
@@ -225,6 +249,8 @@ template <typename T>
 hipError_t launch_inverse_sweepg(const LevelArgs<T>& a, int levels, int ka, int R, bool fma, hipStream_t st);
 template <typename T>
 hipError_t launch_forward_multi(const MultiArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
+template <typename T>
+hipError_t launch_forward_stream(const StreamArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
 template <typename T>
 hipError_t launch_inverse_multi(const MultiArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
 template <typename T>
