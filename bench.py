@@ -114,8 +114,7 @@ def parse(argv=None):
                         "outputs rotated too); 1 = one set (the round-1..3 method)")
     p.add_argument("--rotate-outputs", action="store_true", help="explicit --rotate R: rotate the outputs too")
     p.add_argument("--overlap-steps", action="store_true",
-                   help="experiment: pipeline step i+1's forward with step i's inverse on two contexts "
-                        "(needs --rotate >= 2 --rotate-outputs; prints one line, no kernel roofline)")
+                   help="pipeline step i+1's forward with step i's inverse on two contexts (rotated buffer sets)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--dry-run", action="store_true",
@@ -398,7 +397,7 @@ class Part:
 
 
 def measure_overlap(torch, dist, world, pt, eng_i, stream_i, flags, steps, warmup, settle_s, use_graph=True):
-    """Experiment (`--overlap-steps`): consecutive steps pipelined over two contexts on two streams --
+    """Step schedule `overlap-steps`: consecutive steps pipelined over two contexts on two streams --
     every forward on the part's context / stream F, every inverse on context I / stream I, step i's
     inverse after its forward (event), step i's forward after step i - R's inverse (the buffer set it
     overwrites), R >= 2 rotated output sets.  So step i + 1's forward overlaps step i's inverse; each
@@ -407,7 +406,7 @@ def measure_overlap(torch, dist, world, pt, eng_i, stream_i, flags, steps, warmu
     on stream F around them, stream I joined back)."""
     nat, lib, w, J, N, B = pt.nat, pt.lib, pt.w, pt.J, pt.N, pt.rows
     R = pt.rotate
-    assert R >= 2 and pt.pipeline == "fwd+inv", "--overlap-steps needs --rotate >= 2 --rotate-outputs, fwd+inv"
+    assert R >= 2 and pt.pipeline == "fwd+inv", "overlapped steps need >= 2 buffer sets (outputs too) and fwd+inv"
     p = lambda t: c_void_p(t.data_ptr())  # noqa: E731
     fwd = lib.vw_modwt_forward_f32 if pt.f32 else lib.vw_modwt_forward_f64
     inv = lib.vw_modwt_inverse_f32 if pt.f32 else lib.vw_modwt_inverse_f64
@@ -521,6 +520,11 @@ def measure(torch, dist, world, wl, flags, mode, steps, warmup, settle_s, events
     Returns ((device_elapsed_s, host_elapsed_s), settle (s, steps), {family: (total_ms, launches)},
     timed steps sampled, {pass: wall ms per sampled step across parts}).
     """
+    if getattr(wl, "overlap", None):
+        eng_i, stream_i = wl.overlap
+        el = measure_overlap(torch, dist, world, wl.parts[0], eng_i, stream_i, flags, steps, warmup, settle_s,
+                             mode != "direct")
+        return (el, el), (settle_s, 0), {}, 0, {}
     parts = wl.parts
     main = torch.cuda.current_stream()
     fns = [pt.step_fn(flags) for pt in parts]
@@ -718,23 +722,16 @@ def run(args, world, rank, local):
     x_bytes = rows * N * esz
     R = args.rotate or max(2, -(-(512 << 20) // max(x_bytes, 1)))
     rot = (R, bool(args.rotate_outputs or not args.rotate))
-    if args.overlap_steps:
-        wl = Workload(engines[:1], streams[:1], w, J, rows, N, dtype, pipeline, start, torch, *rot)
-        ei = vw.Engine(local)
-        si = torch.cuda.Stream(device=dev)
-        el = measure_overlap(torch, dist, world, wl.parts[0], ei, si, flags, args.steps, args.warmup, args.settle,
-                             args.launch != "direct")
-        el = max_over_ranks(torch, dist, world, el, dev)
-        check = verify(torch, wl, w, J, pipeline, flags, nat)
-        if rank == 0:
-            print(json.dumps({"experiment": "overlap-steps", "value": round(Bg * N * args.steps / el / 1e6, 2),
-                              "unit": "Msamples/s", "n_gpus": world, "ms_per_step": round(el / args.steps * 1e3, 4),
-                              "batch_per_gpu": rows, "buffer_sets": args.rotate, "check": check}), flush=True)
-        if world > 1:
-            dist.barrier()
-            dist.destroy_process_group()
-        return
+    # Step schedule: `overlap` pipelines consecutive steps over two contexts (step i+1's forward beside step
+    # i's inverse, measure_overlap); otherwise the K contexts above split the rows.
+    overlap = bool(args.overlap_steps) and pipeline == "fwd+inv"
+    if overlap:
+        K = 1
+        engines, streams = engines[:1], streams[:1]
+        rot = (max(rot[0], 2), True)
+    ov = (vw.Engine(local), torch.cuda.Stream(device=dev)) if overlap else None
     wl = Workload(engines, streams, w, J, rows, N, dtype, pipeline, start, torch, *rot)
+    wl.overlap = ov
     footprint = sum(pt.footprint() for pt in wl.parts)
     (elapsed, host_elapsed), (settle_s, settle_steps), fams, sampled, pass_ms = measure(
         torch, dist, world, wl, flags, args.launch, args.steps, args.warmup, args.settle, events)
@@ -760,7 +757,7 @@ def run(args, world, rank, local):
     # timed once more by ONE context over the same rows (after the headline's timed region, same
     # graph method).  With K = 1 the headline's own launches are used.
     kfams, ksampled, kpass_ms = fams, sampled, pass_ms
-    if K > 1 and events:
+    if (K > 1 or overlap) and events:
         wk1 = Workload(engines[:1], streams[:1], w, J, rows, N, dtype, pipeline, start, torch, *rot)
         _, _, kfams, ksampled, kpass_ms = measure(torch, dist, world, wk1, flags, args.launch, args.steps,
                                                   args.warmup, min(args.settle, 0.5), events)
@@ -785,7 +782,8 @@ def run(args, world, rank, local):
                 "algorithmic_bytes_per_launch": pass_bytes[dom], "avg_launch_ms": round(kpass_ms[dom], 5),
                 "duration_from": ("HIP event nodes around every launch of the sampled timed steps"
                                   + (f" of a one-context timing of the same {rows} rows (the headline's "
-                                     f"{K} contexts overlap their launches)" if K > 1 else "")),
+                                     f"{'overlapped steps' if overlap else f'{K} contexts'} overlap their "
+                                     f"launches)" if (K > 1 or overlap) else "")),
                 "kernels": kkernels,
                 # also the fraction of what a plain copy kernel reaches on this GPU
                 "copy_ref_GBps": COPY_GBS, "copy_frac": round(achieved / COPY_GBS, 4),
@@ -828,6 +826,7 @@ def run(args, world, rank, local):
     weak = None
     if world > 1 and not args.no_weak:
         wk = Workload(engines, streams, w, J, Bg, N, dtype, pipeline, rank * Bg, torch, *rot)
+        wk.overlap = ov
         (wel, _), _, _, _, _ = measure(torch, dist, world, wk, flags, args.launch, args.steps, args.warmup,
                                        min(args.settle, 0.3), False)
         wel = max_over_ranks(torch, dist, world, wel, dev)
@@ -866,7 +865,10 @@ def run(args, world, rank, local):
                 "wavelet": wname, "levels": J, "global_batch": Bg, "batch_per_gpu": rows, "signal_length": N,
                 "boundary": "PERIODIC", "accumulation": acc_name(args.config, bool(flags & nat.FLAG_FMA)),
                 "parallelism": f"batch-shard x{world} (contiguous row blocks, no collective)"
-                               + (f", {K} contexts per GPU (own stream each, row blocks)" if K > 1 else ""),
+                               + (f", {K} contexts per GPU (own stream each, row blocks)" if K > 1 else "")
+                               + (", consecutive steps pipelined over two contexts (step i+1's forward beside "
+                                  "step i's inverse, one buffer set per step in flight)" if overlap else ""),
+                "schedule": "overlap-steps" if overlap else ("contexts" if K > 1 else "sequential"),
                 "contexts_per_gpu": K,
                 "launch": LAUNCH_DESC[args.launch],
                 "buffer_sets": {"sets": rot[0], "outputs_rotated": rot[1], "device_bytes_per_rank": footprint,

@@ -61,3 +61,52 @@ def test_stream_f32(engine):
         d0, a0 = _run(engine, torch, w, x, 10, fma, stream=False)
         d1, a1 = _run(engine, torch, w, x, 10, fma, stream=True)
         assert torch.equal(d0, d1) and torch.equal(a0, a1)
+
+
+# ---- streaming inverse (vw_device.h k_inverse_stream, VW_INV_STREAM = 512 | 1024 threads): the finest
+# levels streamed right to left, approximation and detail rings per level.  Per output the K4 order
+# (approximation taps, then detail taps, t + l ascending; MultiLevelMODWTTransform.java:576-589), so every
+# output is bit-identical to the per-level path (multi-level tiles + chained sweeps) and, in EXACT mode,
+# to the restatement of vectorwave-core.
+INV_CASES = [  # wavelet, B, N, J
+    (Daubechies.DB8, 2, 1 << 20, 10),   # config 4's block
+    (Daubechies.DB8, 3, 1 << 18, 10),   # several segments per signal
+    (Daubechies.DB4, 5, 1 << 16, 9),
+    (Haar.INSTANCE, 1, 1 << 15, 12),
+    (Symlet.SYM8, 2, 1 << 17, 8),
+    (Coiflet.COIF5, 1, 1 << 17, 6),
+]
+
+
+@pytest.mark.parametrize("threads", [512, 1024])
+@pytest.mark.parametrize("w,B,N,J", INV_CASES, ids=[f"{c[0].name()}-B{c[1]}-N{c[2]}-J{c[3]}" for c in INV_CASES])
+@pytest.mark.parametrize("fma", [False, True], ids=["exact", "fma"])
+def test_inverse_stream_identical_to_per_level_path(engine, w, B, N, J, fma, threads):
+    import torch
+    x = torch.empty((B, N), dtype=torch.float64, device="cuda")
+    engine.fill_uniform(x, 13)
+    m = vw.BatchMODWT.multiLevelAoS(w, x, J, fma=fma)
+    y0 = vw.BatchMODWT.inverseMultiLevelAoS(w, m.detailPerLevel, m.finalApprox, fma=fma)
+    with engine.options(VW_INV_STREAM=threads):
+        y1 = vw.BatchMODWT.inverseMultiLevelAoS(w, m.detailPerLevel, m.finalApprox, fma=fma)
+    torch.cuda.synchronize()
+    assert torch.equal(y0, y1), float((y0 - y1).abs().max())
+    if not fma and N <= 1 << 18:
+        d = m.detailPerLevel[:, B - 1].cpu().numpy()
+        a = m.finalApprox[B - 1].cpu().numpy()
+        y_ref = O.reconstruct(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC, w.wavelet_id)
+        assert np.array_equal(y1[B - 1].cpu().numpy(), y_ref)
+
+
+def test_inverse_stream_f32(engine):
+    import torch
+    w = Daubechies.DB8
+    x = torch.empty((4, 1 << 18), dtype=torch.float32, device="cuda")
+    engine.fill_uniform(x, 5)
+    for fma in (False, True):
+        m = vw.BatchMODWT.multiLevelAoS(w, x, 10, fma=fma)
+        y0 = vw.BatchMODWT.inverseMultiLevelAoS(w, m.detailPerLevel, m.finalApprox, fma=fma)
+        with engine.options(VW_INV_STREAM=512):
+            y1 = vw.BatchMODWT.inverseMultiLevelAoS(w, m.detailPerLevel, m.finalApprox, fma=fma)
+        torch.cuda.synchronize()
+        assert torch.equal(y0, y1)

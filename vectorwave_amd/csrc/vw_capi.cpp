@@ -74,6 +74,7 @@ struct Tuning {
   int inv_persist = 0;           // VW_INV_PERSIST=1: persistent two-region inverse (k_inverse_persist)
   int dma_nt = 0;                // VW_DMA_NT=1: non-temporal LDS-DMA of signal rows (persistent kernels)
   int fwd_stream = 0;            // VW_FWD_STREAM=1: streaming multi-level forward for long PERIODIC signals
+  int inv_stream = 0;            // VW_INV_STREAM=512|1024: streaming multi-level inverse (threads per workgroup)
   int fwd_tile = 0;        // VW_FWD_TILE: per-level forward tile (0 = default)
   bool multi = true;       // VW_MULTI=0: one launch per level on the long-signal path
   int multi_div = 4;       // VW_MULTI_DIV: reach bound of a level group = tile / div
@@ -122,6 +123,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_INV_PERSIST") t.inv_persist = v < 0 ? d.inv_persist : v;
   else if (k == "VW_DMA_NT") t.dma_nt = v < 0 ? d.dma_nt : v;
   else if (k == "VW_FWD_STREAM") t.fwd_stream = v < 0 ? d.fwd_stream : v;
+  else if (k == "VW_INV_STREAM") t.inv_stream = v < 0 ? d.inv_stream : v;
   else if (k == "VW_FWD_TILE") t.fwd_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI") t.multi = v < 0 ? d.multi : v != 0;
   else if (k == "VW_MULTI_DIV") t.multi_div = v <= 0 ? d.multi_div : v;
@@ -161,7 +163,7 @@ static const char* const kTuningKeys[] = {
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
     "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8",
-    "VW_INV_PERSIST", "VW_MULTI_XCD", "VW_DMA_NT", "VW_FWD_STREAM"};
+    "VW_INV_PERSIST", "VW_MULTI_XCD", "VW_DMA_NT", "VW_FWD_STREAM", "VW_INV_STREAM"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -855,6 +857,55 @@ static int stream_plan(const std::vector<LevelDesc>& lv, int j, int J, int L, in
   return g;
 }
 
+// Streaming inverse plan (vw_device.h k_inverse_stream) for levels 1..g: per level an approximation ring
+// and a detail ring of history (L-1)*s + one chunk (C = threads * V samples; DMA-fed rings a multiple of
+// 64 vectors); the most levels whose rings fit one workgroup's LDS.  Returns g (0: not applicable).
+template <typename T>
+static int inv_stream_plan(const std::vector<LevelDesc>& lv, int J, int L, int64_t N, int64_t B, int cus,
+                           int threads, InvStreamArgs<T>* a) {
+  constexpr int V = vec_width<T>();
+  if (threads != 512 && threads != 1024) return 0;
+  const int64_t C = (int64_t)threads * V;
+  if (N % C != 0 || N < 8 * C) return 0;
+  const int64_t budget = kLdsBytes / (int64_t)sizeof(T);
+  int g = 0;
+  int64_t used = 0, hist = 0;
+  int ca[kMaxGroup], cd[kMaxGroup];
+  while (g < J && g < kMaxGroup && lv[g].mode == kHaloPeriodic && lv[g].use_d && lv[g].dir_a == 1 &&
+         lv[g].dir_d == 1 && lv[g].off_a == 0 && lv[g].off_d == 0) {
+    const int64_t h = (int64_t)(L - 1) * lv[g].s;
+    const int64_t dcap = round_up(h + C, 64 * V);
+    // the approximation ring of the group's top level is DMA-fed too; below it written by the level above
+    const int64_t acap_dma = round_up(h + C, 64 * V), acap = round_up(h + C, V);
+    // with this level as the new top, the previous top's ring no longer needs the DMA rounding
+    const int64_t prev_fix = g > 0 ? (round_up((int64_t)(L - 1) * lv[g - 1].s + C, V) - ca[g - 1]) : 0;
+    if (used + prev_fix + dcap + acap_dma > budget) break;
+    used += prev_fix + dcap + acap_dma;
+    if (g > 0) ca[g - 1] = (int)acap;
+    ca[g] = (int)acap_dma;
+    cd[g] = (int)dcap;
+    hist += h;
+    ++g;
+    (void)acap;
+  }
+  if (g < 2) return 0;
+  const int64_t warm = round_up(hist, C);
+  if (warm > N) return 0;
+  int seg = 1;
+  while (B * seg < cus && N / (2 * seg) >= 4 * C && (N / (2 * seg)) % C == 0) seg *= 2;
+  if (a) {
+    a->g = g; a->N = (int)N; a->B = B; a->s0 = lv[0].s; a->C = (int)C;
+    a->seg = seg; a->seglen = (int)(N / seg); a->warm = (int)warm;
+    int64_t off = 0;
+    for (int k = 0; k < g; ++k) {
+      // (after the loop ca[k] for k < g-1 holds the plain capacity of a ring written by the level above)
+      a->cap_a[k] = ca[k]; a->off_a[k] = (int)off; off += ca[k];
+      a->cap_d[k] = cd[k]; a->off_d[k] = (int)off; off += cd[k];
+    }
+  }
+  return g;
+}
+
 // Level groups of the per-level path (vw_device.h k_forward_multi / k_inverse_multi): from level 1
 // up, consecutive PERIODIC levels run as one multi-level tile launch while their combined reach
 // sum((L-1)*s_j) stays within a quarter of the tile (the redundant arithmetic).  groups[j-1] = size
@@ -1439,11 +1490,38 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       for (int k = 0; k < groups[j - 1]; ++k) ext += round_up((int64_t)(L - 1) * lv[j - 1 + k].s, V);
       if ((mtile + ext) / V <= (int64_t)kMultiInvNI * 256) start_of[j + groups[j - 1] - 1] = j;
     }
-    std::vector<char> in_group(J + 1, 0);  // levels inside a multi-level tile group
+    // streaming inverse of levels 1..gs (VW_INV_STREAM): replaces the multi-level groups it covers
+    InvStreamArgs<T> isa;
+    memset(&isa, 0, sizeof(isa));
+    int gs = 0;
+    if (tu.inv_stream && !pair && boundary == VW_PERIODIC && !thr && has_unrolled_taps(L) && L <= tu.unroll_max &&
+        aligned16(details) && aligned16(y) && aligned16(approx))
+      gs = inv_stream_plan<T>(lv, J, L, N, B, c->cus, tu.inv_stream, &isa);
+    if (gs >= J) gs = 0;  // (the coarsest approximation must come from a level above: keep it simple)
+    for (int e = 1; gs && e <= J; ++e)
+      if (start_of[e] > 0 && start_of[e] <= gs) start_of[e] = 0;
+    std::vector<char> in_group(J + 1, 0);  // levels inside a multi-level tile group or the stream
     for (int e = 1; e <= J; ++e)
       for (int k = start_of[e]; start_of[e] > 0 && k <= e; ++k) in_group[k] = 1;
+    for (int k = 1; k <= gs; ++k) in_group[k] = 1;
     for (int j = J; j >= 1; --j) {
       T* const nxt = (cur == tmp[0]) ? tmp[1] : tmp[0];  // never the level's own input
+      if (gs && j == gs && cur && aligned16(cur)) {
+        isa.src_a = cur;
+        for (int k = 0; k < gs; ++k) isa.src_d[k] = details + (size_t)k * plane;
+        isa.out = y;
+        isa.taps = L; isa.dma_nt = tu.dma_nt;
+        copy_taps(isa.lo, lo, L);
+        copy_taps(isa.hi, hi, L);
+        int lds = 0;
+        for (int k = 0; k < gs; ++k) lds += isa.cap_a[k] + isa.cap_d[k];
+        lds *= (int)sizeof(T);
+        LaunchTimer lt(c, "inverse_level");
+        hipError_t e = launch_inverse_stream<T>(isa, lds, fma, c->stream);
+        if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse stream launch failed: %s", hipGetErrorString(e));
+        cur = y;
+        break;
+      }
       // streaming deep group with top level j: the lowest jl whose group jl..j fits the LDS budget
       if (!pair && boundary == VW_PERIODIC && !in_group[j] && aligned16(cur) && aligned16(details) &&
           aligned16(y) && deep_plan<T>(tu, lv, j, j, L, N, true, nullptr)) {

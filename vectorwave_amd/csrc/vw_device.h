@@ -2364,6 +2364,147 @@ __global__ void __launch_bounds__(kStreamThreads) k_forward_stream(const StreamA
 }
 
 // ---------------------------------------------------------------------------------------------
+// Streaming multi-level inverse for long PERIODIC signals (MultiLevelMODWTTransform.reconstruct
+// :339-349 with the K4 sum of :576-589 per level: all approximation taps, then all detail taps, t + l
+// ascending).  The mirror of k_forward_stream: one workgroup streams one segment of one signal from
+// right to left in chunks of C samples (one vector per thread); the finest g levels run once per chunk,
+// coarsest first.  Level k (level jb + k) reads its approximation input from ring A_k and its detail row
+// from ring D_k at t + i*s_k (right reach H_k = (L-1)*s_k) and writes a_{jb+k-1} into A_{k-1} (level 0:
+// to HBM).  A_{g-1} and every D_k are fed by LDS-DMA one chunk ahead, each issued as soon as the level
+// that reads the ring has finished the current chunk (ring capacity H_k + C suffices); every wave waits
+// for exactly its own DMA of the ring a level needs (counts derived below), then the level's barrier.
+// Chunk c covers positions [T_c, T_c + C), T_c = q0 + seglen + warm - (c+1)*C (mod N); a ring slot is
+// base_c + (t - T_c) mod capacity, base_{c+1} = base_c - C.  The first warm / C chunks lie right of the
+// segment and are not stored (the reach argument of k_forward_stream, mirrored).
+template <typename T, int L, bool FMA, int S>
+__device__ __forceinline__ void stream_inv_window(const T* ring, int cap, int base, const T* f, T (&acc)[VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  static_for<0, (L + kWinTaps - 1) / kWinTaps>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * kWinTaps;
+    constexpr int I1 = (I0 + kWinTaps < L) ? I0 + kWinTaps : L;
+    constexpr int A = floor_div(I0 * S, V) * V;
+    constexpr int E = (floor_div(V - 1 + (I1 - 1) * S, V) + 1) * V;
+    constexpr int NE = E - A;
+    T w[NE];
+#pragma unroll
+    for (int k = 0; k < NE / V; ++k) {
+      const vec v = *reinterpret_cast<const vec*>(ring + ring_slot<T>(base + A + k * V, cap));
+#pragma unroll
+      for (int e = 0; e < V; ++e) w[k * V + e] = v[e];
+    }
+#pragma unroll
+    for (int i = I0; i < I1; ++i) vmadd<FMA>(acc, &w[i * S - A], f[i]);
+  });
+}
+
+template <typename T, int L, bool FMA>
+__device__ __forceinline__ void stream_inv_branch(const T* ring, int cap, int base, int s, const T* f,
+                                                  T (&acc)[VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  if (s == 1) {
+    stream_inv_window<T, L, FMA, 1>(ring, cap, base, f, acc);
+  } else if (V == 4 && s == 2) {
+    stream_inv_window<T, L, FMA, 2>(ring, cap, base, f, acc);
+  } else {
+#pragma unroll
+    for (int i = 0; i < L; ++i) {  // s a multiple of V: aligned 16-byte reads
+      const vec v = *reinterpret_cast<const vec*>(ring + ring_slot<T>(base + i * s, cap));
+      vmadd<FMA>(acc, v, f[i]);
+      if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < V; ++e) asm volatile("" : "+v"(acc[e]));  // the branch's sum completes here
+}
+
+template <typename T, int L, bool FMA>
+__global__ void __launch_bounds__(1024) k_inverse_stream(const InvStreamArgs<T> p) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  T* const lds = reinterpret_cast<T*>(smem);
+  const long long b = blockIdx.x / p.seg;
+  const int sg = blockIdx.x % p.seg;
+  if (b >= p.B) return;
+  const int N = p.N, C = p.C, g = p.g;
+  const int u = threadIdx.x * V;
+  const int nc = (p.warm + p.seglen) / C;
+  const int wc = p.warm / C;
+  const size_t row = (size_t)b * (size_t)N;
+  const bool nt = p.dma_nt != 0;
+  const int lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  auto wrapN = [&](int q) { return q - (q >= N ? N : 0); };  // q < 2N
+  // one DMA instruction per wave: this wave's 64 vectors of chunk (Tc, base) of a row into a ring
+  auto dma = [&](int ring_off, int cap, int base, const T* __restrict__ src, int Tc) {
+    int sl = base + wv * 64 * V;
+    sl -= sl >= cap ? cap : 0;
+    lds_dma16((unsigned)(uintptr_t)(lds + ring_off + sl), src + row + wrapN(Tc + (wv * 64 + lane) * V), nt);
+  };
+  int T0 = (int)(((long long)sg * p.seglen + p.seglen + p.warm - C) % N);  // T_0
+  int ba[kMaxGroup], bd[kMaxGroup];
+#pragma unroll
+  for (int k = 0; k < kMaxGroup; ++k) { ba[k] = 0; bd[k] = 0; }
+  auto next_base = [&](int bs, int cap) { bs -= C; return bs + (bs < 0 ? cap : 0); };
+  // prologue: chunk 0 of every DMA-fed ring
+  dma(p.off_a[g - 1], p.cap_a[g - 1], 0, p.src_a, T0);
+  for (int k = 0; k < g; ++k) dma(p.off_d[k], p.cap_d[k], 0, p.src_d[k], T0);
+  wait_vmem();
+  int Tc = T0;
+  for (int c = 0; c < nc; ++c) {
+    const bool more = c + 1 < nc;
+    const bool st_prev = c - 1 >= wc;  // chunk c-1 stored y (one store per wave)
+    int Tn = Tc - C;                   // T_{c+1}
+    Tn += Tn < 0 ? N : 0;
+    for (int k = g - 1; k >= 0; --k) {
+      if (c >= 1) {
+        // vector-memory operations this wave issued after the DMA level k needs (see the schedule below)
+        int X;
+        if (k == g - 1) X = g - 2 + (st_prev ? 1 : 0);
+        else if (k >= 1) X = k + (st_prev ? 1 : 0) + ((more && k <= g - 3) ? g - 1 - k : 0);
+        else X = (more && g >= 3) ? g - 1 : 0;
+        wait_vmcnt_rt(X);
+      }
+      lds_barrier();  // A_k / D_k hold chunk c; every read of the ring slots the DMAs below refill is done
+      // schedule: B(g-1): D_0(c) [c >= 1]; B(g-2): A_{g-1}(c+1), D_{g-1}(c+1); B(k <= g-3): D_{k+1}(c+1)
+      if (k == g - 1) {
+        if (c >= 1) dma(p.off_d[0], p.cap_d[0], bd[0], p.src_d[0], Tc);
+      } else if (more) {
+        if (k == g - 2) {
+          dma(p.off_a[g - 1], p.cap_a[g - 1], next_base(ba[g - 1], p.cap_a[g - 1]), p.src_a, Tn);
+          dma(p.off_d[g - 1], p.cap_d[g - 1], next_base(bd[g - 1], p.cap_d[g - 1]), p.src_d[g - 1], Tn);
+        } else {
+          dma(p.off_d[k + 1], p.cap_d[k + 1], next_base(bd[k + 1], p.cap_d[k + 1]), p.src_d[k + 1], Tn);
+        }
+      }
+      const int s = p.s0 << k;
+      T acc[V];
+#pragma unroll
+      for (int e = 0; e < V; ++e) acc[e] = T(0);
+      stream_inv_branch<T, L, FMA>(lds + p.off_a[k], p.cap_a[k], ba[k] + u, s, p.lo, acc);
+      stream_inv_branch<T, L, FMA>(lds + p.off_d[k], p.cap_d[k], bd[k] + u, s, p.hi, acc);
+      vec o;
+#pragma unroll
+      for (int e = 0; e < V; ++e) o[e] = acc[e];
+      if (k > 0) {
+        *reinterpret_cast<vec*>(lds + p.off_a[k - 1] + ring_slot<T>(ba[k - 1] + u, p.cap_a[k - 1])) = o;
+      } else if (c >= wc) {
+        stream_store<VW_INV_STORE_AUX, vec>(p.out + row, wrapN(Tc + u) / V, o);
+      }
+    }
+    for (int k = 0; k < kMaxGroup; ++k) {
+      if (k < g) {
+        ba[k] = next_base(ba[k], p.cap_a[k]);
+        bd[k] = next_base(bd[k], p.cap_d[k]);
+      }
+    }
+    Tc = Tn;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Multi-level tiles for long PERIODIC signals (host: vw_capi.cpp level_groups).  One workgroup runs
 // a group of consecutive levels over one tile of one signal; the intermediate approximations stay
 // in LDS.  Periodic convolution commutes with shifts, so a level evaluated at a position v outside

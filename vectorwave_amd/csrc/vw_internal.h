@@ -192,6 +192,27 @@ struct StreamArgs {
   T hi[kMaxTaps];
 };
 
+// Streaming multi-level inverse (PERIODIC sequential sums; vw_device.h k_inverse_stream): the finest g
+// levels of a long signal in one launch, streamed right to left; per level an LDS ring of its
+// approximation input (the coarsest one DMA-fed, the others written by the level above) and one of its
+// detail row (DMA-fed), each holding the (L-1)*s samples of history plus one chunk.
+template <typename T>
+struct InvStreamArgs {
+  const T* src_a;             // approximation input of level jb+g-1 [B][N]
+  const T* src_d[kMaxGroup];  // d of level jb+k [B][N]
+  T* out;                     // a_{jb-1} (y when jb = 1) [B][N]
+  long long B;
+  int N, g, s0;               // levels, spacing of level jb
+  int C;                      // chunk samples (threads * V)
+  int seg, seglen, warm;      // as StreamArgs; the warm-up lies to the RIGHT of the segment
+  int cap_a[kMaxGroup], off_a[kMaxGroup];
+  int cap_d[kMaxGroup], off_d[kMaxGroup];
+  int dma_nt;
+  int taps;
+  T lo[kMaxTaps];
+  T hi[kMaxTaps];
+};
+
 // WaveletDenoiser threshold methods (core/denoising/WaveletDenoiser.java:588-622) and the per-launch
 // constants of the threshold kernels (vw_sigma.h).
 enum ThrMethod { kThrUniversal = 0, kThrSure = 1, kThrMinimax = 2, kThrBayes = 3, kThrFixed = 4 };
@@ -251,6 +272,8 @@ template <typename T>
 hipError_t launch_forward_multi(const MultiArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
 template <typename T>
 hipError_t launch_forward_stream(const StreamArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
+template <typename T>
+hipError_t launch_inverse_stream(const InvStreamArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
 template <typename T>
 hipError_t launch_inverse_multi(const MultiArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
 template <typename T>
