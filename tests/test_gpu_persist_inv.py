@@ -115,3 +115,35 @@ def test_persist_declines_outside_its_contract(engine):
     engine.set_option("VW_INV_PERSIST", -1)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("B", [4096, 700, 512])
+def test_persistent_forward_register_prefetch_identical(engine, B):
+    """k_forward_persist with the next row prefetched into registers from level 1 (VW_FWD_PF=1) instead of
+    DMA'd during level J: the same outputs bit for bit (EXACT and FMA), every row."""
+    import torch
+    from ctypes import c_void_p
+    w = Daubechies.DB4
+    N, J = 4096, 6
+    P = lambda t: c_void_p(t.data_ptr())  # noqa: E731
+    x = torch.empty((B, N), dtype=torch.float64, device="cuda")
+    engine.fill_uniform(x, 3)
+    lo, hi = w.lowPassDecomposition(), w.highPassDecomposition()
+    engine.bind_torch_stream()
+    for flags in (0, nat.FLAG_FMA):
+        outs = []
+        for pf in (0, 1):
+            det = torch.empty((J, B, N), dtype=torch.float64, device="cuda")
+            app = torch.empty((B, N), dtype=torch.float64, device="cuda")
+            with engine.options(VW_FWD_PF=pf):
+                assert engine.lib.vw_modwt_forward_f64(engine.ctx, P(x), B, N, N, nat.taps_array(lo),
+                                                       nat.taps_array(hi), len(lo), w.wavelet_id, nat.PERIODIC, J,
+                                                       flags, P(det), P(app)) == 0, nat.last_error()
+            outs.append((det, app))
+        torch.cuda.synchronize()
+        assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    if B == 700:   # EXACT rows across persistent workgroups against the restatement
+        d, a = outs[0]
+        for b in (0, 699):
+            d_ref, a_ref = O.decompose(x[b].cpu().numpy(), lo, hi, O.PERIODIC, J, core=False)
+            assert np.abs(d[:, b].cpu().numpy() - d_ref).max() <= 1e-12

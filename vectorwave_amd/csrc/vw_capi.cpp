@@ -75,6 +75,7 @@ struct Tuning {
   int dma_nt = 0;                // VW_DMA_NT=1: non-temporal LDS-DMA of signal rows (persistent kernels)
   int fwd_stream = 0;            // VW_FWD_STREAM=1: streaming multi-level forward for long PERIODIC signals
   int inv_stream = 0;            // VW_INV_STREAM=512|1024: streaming multi-level inverse (threads per workgroup)
+  int fwd_pf = 0;                // VW_FWD_PF=1: persistent forward prefetches the next row into registers
   int fwd_tile = 0;        // VW_FWD_TILE: per-level forward tile (0 = default)
   bool multi = true;       // VW_MULTI=0: one launch per level on the long-signal path
   int multi_div = 4;       // VW_MULTI_DIV: reach bound of a level group = tile / div
@@ -124,6 +125,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_DMA_NT") t.dma_nt = v < 0 ? d.dma_nt : v;
   else if (k == "VW_FWD_STREAM") t.fwd_stream = v < 0 ? d.fwd_stream : v;
   else if (k == "VW_INV_STREAM") t.inv_stream = v < 0 ? d.inv_stream : v;
+  else if (k == "VW_FWD_PF") t.fwd_pf = v < 0 ? d.fwd_pf : v;
   else if (k == "VW_FWD_TILE") t.fwd_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI") t.multi = v < 0 ? d.multi : v != 0;
   else if (k == "VW_MULTI_DIV") t.multi_div = v <= 0 ? d.multi_div : v;
@@ -163,7 +165,7 @@ static const char* const kTuningKeys[] = {
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
     "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8",
-    "VW_INV_PERSIST", "VW_MULTI_XCD", "VW_DMA_NT", "VW_FWD_STREAM", "VW_INV_STREAM"};
+    "VW_INV_PERSIST", "VW_MULTI_XCD", "VW_DMA_NT", "VW_FWD_STREAM", "VW_INV_STREAM", "VW_FWD_PF"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -876,17 +878,17 @@ static int inv_stream_plan(const std::vector<LevelDesc>& lv, int J, int L, int64
     const int64_t h = (int64_t)(L - 1) * lv[g].s;
     const int64_t dcap = round_up(h + C, 64 * V);
     // the approximation ring of the group's top level is DMA-fed too; below it written by the level above
-    const int64_t acap_dma = round_up(h + C, 64 * V), acap = round_up(h + C, V);
+    const int64_t acap_dma = round_up(h + C, 64 * V);
     // with this level as the new top, the previous top's ring no longer needs the DMA rounding
-    const int64_t prev_fix = g > 0 ? (round_up((int64_t)(L - 1) * lv[g - 1].s + C, V) - ca[g - 1]) : 0;
+    const int64_t prev_plain = g > 0 ? round_up((int64_t)(L - 1) * lv[g - 1].s + C, V) : 0;
+    const int64_t prev_fix = g > 0 ? prev_plain - ca[g - 1] : 0;
     if (used + prev_fix + dcap + acap_dma > budget) break;
     used += prev_fix + dcap + acap_dma;
-    if (g > 0) ca[g - 1] = (int)acap;
+    if (g > 0) ca[g - 1] = (int)prev_plain;
     ca[g] = (int)acap_dma;
     cd[g] = (int)dcap;
     hist += h;
     ++g;
-    (void)acap;
   }
   if (g < 2) return 0;
   const int64_t warm = round_up(hist, C);
@@ -1114,6 +1116,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     a.validate = validate; a.bad = c->bad;
     a.rev = tu.fwd_rev;
     a.dma_nt = tu.dma_nt;
+    a.pf_regs = tu.fwd_pf;
     for (int j = 0; j < J; ++j) a.hist[j] = hist ? hist[j] : nullptr;
     a.hist_update = hist_update ? 1 : 0;
     a.taps = L;

@@ -922,20 +922,38 @@ k_forward_persist(const FwdArgs<T> p) {
   long long b = blockIdx.x;
   if (b >= p.B) return;
   int cur = 0;
-  dma_row<T>(B0, p.x + b * p.ldx, nvec, p.dma_nt != 0);
-  wait_vmem();
+  // p.pf_regs: the next signal's row is loaded into registers from level 1 on (a whole signal of time to
+  // land) and written into the free buffer after level J; else it is DMA'd during level J.
+  const bool pfr = p.pf_regs != 0;
+  if (pfr) {
+    T x0[NV][V];
+    load_row_regs<T, NV>(x0, p.x + b * p.ldx, N, nvec, true, false);
+    regs_to_level<T, L, NV>(B0, x0, nvec, N, p.lv[0], p.npow2, (const T*)nullptr);
+  } else {
+    dma_row<T>(B0, p.x + b * p.ldx, nvec, p.dma_nt != 0);
+    wait_vmem();
+  }
   for (;;) {
     T* X = cur ? B1 : B0;
     T* Y = cur ? B0 : B1;
     lds_barrier();  // the row is in X (every wave's share); every read of the previous signal done
-    const LevelDesc lv0 = p.lv[0];
-    fill_halo(X, N, lv0.hl, lv0.hr, lv0.mode, p.npow2, (const T*)nullptr, 0);
+    if (!pfr) {
+      const LevelDesc lv0 = p.lv[0];
+      fill_halo(X, N, lv0.hl, lv0.hr, lv0.mode, p.npow2, (const T*)nullptr, 0);
+    }
     const long long bn = b + G;
     T areg[NV][V];
+    // register prefetch of the next row, issued once per signal outside the level loop (a load under a
+    // per-level condition makes the compiler carry the registers through loop phis and wait vmcnt(0)
+    // at every level); past the last signal it re-reads a valid row that is never used
+    T xreg[NV][V];
+    if (pfr) load_row_regs<T, NV>(xreg, p.x + min(bn, p.B - 1) * p.ldx, N, nvec, true, false);
     for (int j = 1; j <= p.J; ++j) {
       const LevelDesc lv = p.lv[j - 1];
       lds_barrier();  // X = level input + halo; every read of Y (previous level) done
-      if (j == p.J && bn < p.B) dma_row<T>(Y, p.x + bn * p.ldx, nvec, p.dma_nt != 0);  // next signal -> free buffer
+      if (!pfr && j == p.J && bn < p.B) {
+        dma_row<T>(Y, p.x + bn * p.ldx, nvec, p.dma_nt != 0);  // next signal -> free buffer
+      }
       T* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
       T* aout = (j == p.J) ? p.approx + b * (size_t)N : nullptr;
       fwd_level<T, L, FMA, NV, false>(p, X, nvec, lv, dout, aout, true, 0ull, areg);
@@ -945,7 +963,11 @@ k_forward_persist(const FwdArgs<T> p) {
       }
     }
     if (bn >= p.B) break;
-    wait_vmcnt<2 * NV>();  // this wave's DMA share landed; level J's stores stay in flight
+    if (pfr) {
+      regs_to_level<T, L, NV>(Y, xreg, nvec, N, p.lv[0], p.npow2, (const T*)nullptr);  // Y: unused by level J
+    } else {
+      wait_vmcnt<2 * NV>();  // this wave's DMA share landed; level J's stores stay in flight
+    }
     cur = (cur + p.J) & 1;  // the buffer that was free during level J
     b = bn;
   }

@@ -56,6 +56,7 @@ struct FwdArgs {
   int vec_io;
   int unrolled;         // 1: the tap-unrolled kernel may run (aligned rows, full slabs; vw_capi fused_plan)
   int dma_nt;           // k_forward_persist: non-temporal LDS-DMA of the signal rows
+  int pf_regs;          // k_forward_persist: next row prefetched into registers from level 1 (not DMA'd at level J)
   int validate;         // 1: non-finite check on input and outputs (atomicMin into *bad)
   int rev;              // 1: workgroup g owns signal B-1-g (walk order, see vw_capi.cpp walk_reverse)
   unsigned long long* bad;
