@@ -114,7 +114,8 @@ def parse(argv=None):
                         "outputs rotated too); 1 = one set (the round-1..3 method)")
     p.add_argument("--rotate-outputs", action="store_true", help="explicit --rotate R: rotate the outputs too")
     p.add_argument("--overlap-steps", action="store_true",
-                   help="pipeline step i+1's forward with step i's inverse on two contexts (rotated buffer sets)")
+                   help="pipeline step i+1's forward with step i's inverse on two contexts (rotated buffer sets); "
+                        "default when the rank has <= 2 signals per CU and --contexts is not given")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=6.0, help="target wall time of the CPU baseline sample")
     p.add_argument("--dry-run", action="store_true",
@@ -396,14 +397,15 @@ class Part:
         return step
 
 
-def measure_overlap(torch, dist, world, pt, eng_i, stream_i, flags, steps, warmup, settle_s, use_graph=True):
+def measure_overlap(torch, dist, world, pt, eng_i, stream_i, flags, steps, warmup, settle_s):
     """Step schedule `overlap-steps`: consecutive steps pipelined over two contexts on two streams --
     every forward on the part's context / stream F, every inverse on context I / stream I, step i's
     inverse after its forward (event), step i's forward after step i - R's inverse (the buffer set it
     overwrites), R >= 2 rotated output sets.  So step i + 1's forward overlaps step i's inverse; each
-    step still runs its full forward and inverse.  The K timed steps are recorded into one graph (or
-    issued as direct C-ABI calls, use_graph=False).  Returns device seconds of the K timed steps (events
-    on stream F around them, stream I joined back)."""
+    step still runs its full forward and inverse.  Direct C-ABI calls on the two streams: the same steps
+    recorded into one graph (torch stream capture over both streams) lost the overlap -- 35.6K vs 42.3K
+    Msamples/s at 512 rows (profiles/r04/ab_overlap_graph.log vs ab_overlap_direct_512.log).  Returns
+    device seconds of the K timed steps (events on stream F around them, stream I joined back)."""
     nat, lib, w, J, N, B = pt.nat, pt.lib, pt.w, pt.J, pt.N, pt.rows
     R = pt.rotate
     assert R >= 2 and pt.pipeline == "fwd+inv", "overlapped steps need >= 2 buffer sets (outputs too) and fwd+inv"
@@ -450,28 +452,14 @@ def measure_overlap(torch, dist, world, pt, eng_i, stream_i, flags, steps, warmu
             torch.cuda.synchronize()
     join()
     torch.cuda.synchronize()
-    graph = None
-    if use_graph:
-        # the K timed steps (both streams, their event edges) recorded once into one graph (torch stream
-        # capture from stream F; stream I joins through the events and rejoins before the end)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=sF):
-            for i in range(steps):
-                one(n + i)
-            join()
-        graph.replay()   # first replay (upload) outside the timed region
-        torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(sF)
-    if graph is not None:
-        graph.replay()
-    else:
-        for i in range(steps):
-            one(n + i)
-        join()
+    for i in range(steps):
+        one(n + i)
+    join()
     ev1.record(sF)
     torch.cuda.synchronize()
     if world > 1:
@@ -522,8 +510,7 @@ def measure(torch, dist, world, wl, flags, mode, steps, warmup, settle_s, events
     """
     if getattr(wl, "overlap", None):
         eng_i, stream_i = wl.overlap
-        el = measure_overlap(torch, dist, world, wl.parts[0], eng_i, stream_i, flags, steps, warmup, settle_s,
-                             mode != "direct")
+        el = measure_overlap(torch, dist, world, wl.parts[0], eng_i, stream_i, flags, steps, warmup, settle_s)
         return (el, el), (settle_s, 0), {}, 0, {}
     parts = wl.parts
     main = torch.cuda.current_stream()
@@ -710,9 +697,10 @@ def run(args, world, rank, local):
     # ---- strong scaling (headline): rank r owns rows [start, start + rows) of the global batch
     start, rows = shard_rows(Bg, world, rank)
     # contexts per GPU: K parts of the rank's rows, each on its own context + stream (--contexts; 0 =
-    # policy: 2 from 1024 rows on -- measured on MI355X, db4 4096 x 4096: 43.6-44.0K -> 44.7-45.7K;
-    # 1024 rows: 39.4K -> 44.1K; 512 rows: 37.0K -> 36.1K (profiles/r03/ab_contexts.log))
-    K = args.contexts or (2 if rows >= 1024 else 1)
+    # policy: 2 above 2 signals per CU -- measured on MI355X, db4 4096 x 4096: 43.6-44.0K -> 44.7-45.7K;
+    # 1024 rows: 39.4K -> 44.1K; 512 rows: 37.0K -> 36.1K (profiles/r03/ab_contexts.log); at or below that,
+    # overlapped steps (below))
+    K = args.contexts or (2 if rows > 2 * torch.cuda.get_device_properties(dev).multi_processor_count else 1)
     engines = [vw.Engine.get(local)] + [vw.Engine(local) for _ in range(K - 1)]
     streams = [main] + [torch.cuda.Stream(device=dev) for _ in range(K - 1)]
     # Buffer sets: with one set the same 128 MiB input was re-read every step and stayed in
@@ -724,7 +712,14 @@ def run(args, world, rank, local):
     rot = (R, bool(args.rotate_outputs or not args.rotate))
     # Step schedule: `overlap` pipelines consecutive steps over two contexts (step i+1's forward beside step
     # i's inverse, measure_overlap); otherwise the K contexts above split the rows.
-    overlap = bool(args.overlap_steps) and pipeline == "fwd+inv"
+    # Policy (measured on MI355X, db4 J=6, rotated sets; profiles/r04/ab_overlap_direct_512.log,
+    # ab_overlap_direct_4096.log, ab_overlap_graph.log): at <= 2 signals per CU (the 8-GPU shard of the
+    # headline: 512 rows) the passes are short and each leaves the GPU half idle at its ends, so overlapping
+    # consecutive steps wins (37.7-38.0K -> 42.1-42.4K) while splitting the rows over two contexts loses
+    # (34.9-35.2K); from 1024 rows on two contexts win (42.3K vs 37.3-37.5K at 1024, 42.2-44.2K vs 40.0-40.6K
+    # at 4096).
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    overlap = pipeline == "fwd+inv" and (args.overlap_steps or (not args.contexts and rows <= 2 * cus))
     if overlap:
         K = 1
         engines, streams = engines[:1], streams[:1]
@@ -870,7 +865,8 @@ def run(args, world, rank, local):
                                   "step i's inverse, one buffer set per step in flight)" if overlap else ""),
                 "schedule": "overlap-steps" if overlap else ("contexts" if K > 1 else "sequential"),
                 "contexts_per_gpu": K,
-                "launch": LAUNCH_DESC[args.launch],
+                "launch": ("direct C-ABI calls on two streams, event edges between them (overlapped steps)"
+                           if overlap else LAUNCH_DESC[args.launch]),
                 "buffer_sets": {"sets": rot[0], "outputs_rotated": rot[1], "device_bytes_per_rank": footprint,
                                 "why": "step i works on set i mod R: no step re-reads an input an earlier step left "
                                        "in the 256 MiB Infinity Cache"},

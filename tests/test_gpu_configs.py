@@ -227,24 +227,3 @@ def test_config5_full_batch_65536x8192_f32(engine):
         np.testing.assert_allclose(app[b].double().cpu().numpy(), a_ref, rtol=0, atol=tol)
         np.testing.assert_allclose(y[b].double().cpu().numpy(), y_ref, rtol=0, atol=tol)
     del x, det, app, y
-
-
-@pytest.mark.parametrize("chunk", [64, 3])
-def test_multi_level_tiles_xcd_runs_identical(engine, chunk):
-    """VW_MULTI_XCD (vw_device.h multi_work): the multi-level tile kernels on a 1-D grid of XCD runs of
-    neighbouring tiles, padding workgroups included (3 signals x 128 tiles is not a multiple of 8 runs):
-    the same outputs bit for bit as the 2-D grid, forward and inverse, EXACT and FMA."""
-    import torch
-    w = Daubechies.DB8
-    n, J, B = 1 << 18, 10, 3
-    x = torch.empty((B, n), dtype=torch.float64, device="cuda")
-    engine.fill_uniform(x, 7)
-    for fma in (False, True):
-        m0 = vw.BatchMODWT.multiLevelAoS(w, x, J, fma=fma)
-        y0 = vw.BatchMODWT.inverseMultiLevelAoS(w, m0.detailPerLevel, m0.finalApprox, fma=fma)
-        with engine.options(VW_MULTI_XCD=chunk):
-            m1 = vw.BatchMODWT.multiLevelAoS(w, x, J, fma=fma)
-            y1 = vw.BatchMODWT.inverseMultiLevelAoS(w, m1.detailPerLevel, m1.finalApprox, fma=fma)
-        torch.cuda.synchronize()
-        assert torch.equal(m0.detailPerLevel, m1.detailPerLevel) and torch.equal(m0.finalApprox, m1.finalApprox)
-        assert torch.equal(y0, y1)

@@ -71,16 +71,11 @@ struct Tuning {
   int fwd_buf = 0;         // VW_FWD_BUF=1|2: force one / two forward level buffers (0 = policy)
   bool force_tiled = false;// VW_FORCE_TILED: per-level path even when the fused kernels fit
   int fwd_rev = 0, inv_rev = 0;  // VW_FWD_REV / VW_INV_REV: reverse workgroup -> signal walk
-  int inv_persist = 0;           // VW_INV_PERSIST=1: persistent two-region inverse (k_inverse_persist)
-  int dma_nt = 0;                // VW_DMA_NT=1: non-temporal LDS-DMA of signal rows (persistent kernels)
-  int fwd_stream = 0;            // VW_FWD_STREAM=1: streaming multi-level forward for long PERIODIC signals
-  int inv_stream = 0;            // VW_INV_STREAM=512|1024: streaming multi-level inverse (threads per workgroup)
-  int fwd_pf = 0;                // VW_FWD_PF=1: persistent forward prefetches the next row into registers
+  int dma_nt = -1;               // VW_DMA_NT=0|1: LDS-DMA of signal rows non-temporal; -1 = policy (see forward_impl)
   int fwd_tile = 0;        // VW_FWD_TILE: per-level forward tile (0 = default)
   bool multi = true;       // VW_MULTI=0: one launch per level on the long-signal path
   int multi_div = 4;       // VW_MULTI_DIV: reach bound of a level group = tile / div
   int multi_tile = 0;      // VW_MULTI_TILE: multi-level tile (0 = 16 KiB of samples)
-  int multi_xcd = 0;       // VW_MULTI_XCD: runs of this many neighbouring tiles per XCD (0 = 2-D grid)
   int inv_buf = 0;         // VW_INV_BUF=2: two-buffer sequential inverse (k_inverse_db)
   int inv_tile = 0;        // VW_INV_TILE: per-level inverse tile (0 = 1024)
   int multi_rblk = 1;      // VW_MULTI_RBLK: register-blocked taps in k_inverse_multi
@@ -121,16 +116,11 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_FORCE_TILED") t.force_tiled = v > 0;
   else if (k == "VW_FWD_REV") t.fwd_rev = v < 0 ? 0 : v;
   else if (k == "VW_INV_REV") t.inv_rev = v < 0 ? 0 : v;
-  else if (k == "VW_INV_PERSIST") t.inv_persist = v < 0 ? d.inv_persist : v;
   else if (k == "VW_DMA_NT") t.dma_nt = v < 0 ? d.dma_nt : v;
-  else if (k == "VW_FWD_STREAM") t.fwd_stream = v < 0 ? d.fwd_stream : v;
-  else if (k == "VW_INV_STREAM") t.inv_stream = v < 0 ? d.inv_stream : v;
-  else if (k == "VW_FWD_PF") t.fwd_pf = v < 0 ? d.fwd_pf : v;
   else if (k == "VW_FWD_TILE") t.fwd_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI") t.multi = v < 0 ? d.multi : v != 0;
   else if (k == "VW_MULTI_DIV") t.multi_div = v <= 0 ? d.multi_div : v;
   else if (k == "VW_MULTI_TILE") t.multi_tile = v < 0 ? 0 : v;
-  else if (k == "VW_MULTI_XCD") t.multi_xcd = v < 0 ? d.multi_xcd : v;
   else if (k == "VW_INV_BUF") t.inv_buf = v < 0 ? 0 : v;  // 0 = policy
   else if (k == "VW_INV_TILE") t.inv_tile = v < 0 ? 0 : v;
   else if (k == "VW_MULTI_RBLK") t.multi_rblk = v < 0 ? d.multi_rblk : v;
@@ -165,7 +155,7 @@ static const char* const kTuningKeys[] = {
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
     "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8",
-    "VW_INV_PERSIST", "VW_MULTI_XCD", "VW_DMA_NT", "VW_FWD_STREAM", "VW_INV_STREAM", "VW_FWD_PF"};
+    "VW_DMA_NT"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -822,92 +812,6 @@ static void set_halo_images(LevelDesc& d, int64_t N, int64_t npow2, int V, int t
   d.own = (d.hl <= N && d.hr <= N && d.vs <= threads && (int64_t)d.ve >= (int64_t)(nv - 1) * threads) ? 1 : 0;
 }
 
-// Streaming forward plan (vw_device.h k_forward_stream) from level j: the most consecutive PERIODIC
-// levels whose LDS rings (history (L-1)*s + one chunk of 1024 vectors each; ring 0 a multiple of 64
-// vectors for the DMA) fit one workgroup's LDS; segments so that B * seg fills the CUs.  Returns the
-// group size (0: not applicable).
-template <typename T>
-static int stream_plan(const std::vector<LevelDesc>& lv, int j, int J, int L, int64_t N, int64_t B, int cus,
-                       StreamArgs<T>* a) {
-  constexpr int V = vec_width<T>();
-  constexpr int64_t C = (int64_t)kStreamThreads * V;
-  if (N % C != 0 || N < 8 * C) return 0;
-  const int64_t budget = kLdsBytes / (int64_t)sizeof(T);
-  int g = 0;
-  int64_t used = 0, hist = 0;
-  int cap[kMaxGroup];
-  while (j + g <= J && g < kMaxGroup && lv[j + g - 1].mode == kHaloPeriodic) {
-    const int64_t h = (int64_t)(L - 1) * lv[j + g - 1].s;
-    const int64_t cp = g == 0 ? round_up(h + C, 64 * V) : round_up(h + C, V);
-    if (used + cp > budget) break;
-    cap[g] = (int)cp;
-    used += cp;
-    hist += h;
-    ++g;
-  }
-  if (g < 2) return 0;
-  const int64_t warm = round_up(hist, C);
-  if (warm > N) return 0;
-  int seg = 1;
-  while (B * seg < cus && N / (2 * seg) >= 4 * C && (N / (2 * seg)) % C == 0) seg *= 2;
-  if (a) {
-    a->g = g; a->N = (int)N; a->B = B; a->s0 = lv[j - 1].s;
-    a->seg = seg; a->seglen = (int)(N / seg); a->warm = (int)warm;
-    int64_t off = 0;
-    for (int k = 0; k < g; ++k) { a->cap[k] = cap[k]; a->off[k] = (int)off; off += cap[k]; }
-  }
-  return g;
-}
-
-// Streaming inverse plan (vw_device.h k_inverse_stream) for levels 1..g: per level an approximation ring
-// and a detail ring of history (L-1)*s + one chunk (C = threads * V samples; DMA-fed rings a multiple of
-// 64 vectors); the most levels whose rings fit one workgroup's LDS.  Returns g (0: not applicable).
-template <typename T>
-static int inv_stream_plan(const std::vector<LevelDesc>& lv, int J, int L, int64_t N, int64_t B, int cus,
-                           int threads, InvStreamArgs<T>* a) {
-  constexpr int V = vec_width<T>();
-  if (threads != 512 && threads != 1024) return 0;
-  const int64_t C = (int64_t)threads * V;
-  if (N % C != 0 || N < 8 * C) return 0;
-  const int64_t budget = kLdsBytes / (int64_t)sizeof(T);
-  int g = 0;
-  int64_t used = 0, hist = 0;
-  int ca[kMaxGroup], cd[kMaxGroup];
-  while (g < J && g < kMaxGroup && lv[g].mode == kHaloPeriodic && lv[g].use_d && lv[g].dir_a == 1 &&
-         lv[g].dir_d == 1 && lv[g].off_a == 0 && lv[g].off_d == 0) {
-    const int64_t h = (int64_t)(L - 1) * lv[g].s;
-    const int64_t dcap = round_up(h + C, 64 * V);
-    // the approximation ring of the group's top level is DMA-fed too; below it written by the level above
-    const int64_t acap_dma = round_up(h + C, 64 * V);
-    // with this level as the new top, the previous top's ring no longer needs the DMA rounding
-    const int64_t prev_plain = g > 0 ? round_up((int64_t)(L - 1) * lv[g - 1].s + C, V) : 0;
-    const int64_t prev_fix = g > 0 ? prev_plain - ca[g - 1] : 0;
-    if (used + prev_fix + dcap + acap_dma > budget) break;
-    used += prev_fix + dcap + acap_dma;
-    if (g > 0) ca[g - 1] = (int)prev_plain;
-    ca[g] = (int)acap_dma;
-    cd[g] = (int)dcap;
-    hist += h;
-    ++g;
-  }
-  if (g < 2) return 0;
-  const int64_t warm = round_up(hist, C);
-  if (warm > N) return 0;
-  int seg = 1;
-  while (B * seg < cus && N / (2 * seg) >= 4 * C && (N / (2 * seg)) % C == 0) seg *= 2;
-  if (a) {
-    a->g = g; a->N = (int)N; a->B = B; a->s0 = lv[0].s; a->C = (int)C;
-    a->seg = seg; a->seglen = (int)(N / seg); a->warm = (int)warm;
-    int64_t off = 0;
-    for (int k = 0; k < g; ++k) {
-      // (after the loop ca[k] for k < g-1 holds the plain capacity of a ring written by the level above)
-      a->cap_a[k] = ca[k]; a->off_a[k] = (int)off; off += ca[k];
-      a->cap_d[k] = cd[k]; a->off_d[k] = (int)off; off += cd[k];
-    }
-  }
-  return g;
-}
-
 // Level groups of the per-level path (vw_device.h k_forward_multi / k_inverse_multi): from level 1
 // up, consecutive PERIODIC levels run as one multi-level tile launch while their combined reach
 // sum((L-1)*s_j) stays within a quarter of the tile (the redundant arithmetic).  groups[j-1] = size
@@ -1115,8 +1019,10 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     a.unrolled = a.vec_io && fit && L <= tu.unroll_max;
     a.validate = validate; a.bad = c->bad;
     a.rev = tu.fwd_rev;
-    a.dma_nt = tu.dma_nt;
-    a.pf_regs = tu.fwd_pf;
+    // non-temporal LDS-DMA of the rows: faster at <= 2 signals per CU (512 rows: forward 0.0268 -> 0.0245 ms),
+    // slower on full batches (4096 rows: 0.218-0.225 -> 0.234-0.243 ms; profiles/r04/ab_rotate_default_*.log,
+    // ab_overlap_direct_512.log)
+    a.dma_nt = tu.dma_nt >= 0 ? tu.dma_nt : (B <= 2LL * c->cus ? 1 : 0);
     for (int j = 0; j < J; ++j) a.hist[j] = hist ? hist[j] : nullptr;
     a.hist_update = hist_update ? 1 : 0;
     a.taps = L;
@@ -1190,33 +1096,6 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     const std::vector<int> groups = level_groups(tu, lv, J, L, V, mtile, !validate && !hist);
     for (int j = 1; j <= J; ++j) {
       T* const nxt = (src == tmp[0]) ? tmp[1] : tmp[0];  // never the level's own input
-      // streaming multi-level forward from level j (VW_FWD_STREAM)
-      if (tu.fwd_stream && !validate && !hist && (lda % V) == 0 && aligned16(src) && aligned16(details) &&
-          aligned16(approx) && has_unrolled_taps(L) && L <= tu.unroll_max) {
-        StreamArgs<T> sa;
-        memset(&sa, 0, sizeof(sa));
-        const int g = stream_plan<T>(lv, j, J, L, N, B, c->cus, &sa);
-        if (g >= 2) {
-          const int je = j + g - 1;
-          sa.src = src; sa.lda = lda; sa.taps = L; sa.dma_nt = tu.dma_nt;
-          sa.out = (je == J) ? approx : nxt;
-          for (int k = 0; k < g; ++k) sa.out_d[k] = details + (size_t)(j - 1 + k) * plane;
-          copy_taps(sa.lo, lo, L);
-          copy_taps(sa.hi, hi, L);
-          int lds = 0;
-          for (int k = 0; k < g; ++k) lds += sa.cap[k];
-          lds *= (int)sizeof(T);
-          {
-            LaunchTimer lt(c, "forward_level");
-            hipError_t e = launch_forward_stream<T>(sa, lds, fma, c->stream);
-            if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward stream launch failed: %s", hipGetErrorString(e));
-          }
-          src = sa.out;
-          lda = N;
-          j = je;
-          continue;
-        }
-      }
       // streaming deep group from level j: the longest run j..je within the LDS budget
       if (groups[j - 1] == 1 && !validate && !hist && (lda % V) == 0 && aligned16(src) && aligned16(details) &&
           aligned16(approx) && deep_plan<T>(tu, lv, j, j, L, N, false, nullptr)) {
@@ -1259,7 +1138,6 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
         m.region = (int)round_up(m.ext[0] + mtile + V, V);
         m.vec_io = (N % V == 0) && (lda % V == 0) && al;
         m.taps = L;
-        m.xcd_chunk = tu.multi_xcd;
         copy_taps(m.lo, lo, L);
         copy_taps(m.hi, hi, L);
         {
@@ -1386,32 +1264,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   bool fused = false, fit = false;
   const bool inv_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
   const int inv_nv2 = (tu.inv_nv == 2 && inv_io && L <= 8 && L <= tu.unroll_max && has_unrolled_taps(L)) ? 2 : 0;
-  // Persistent two-region inverse (vw_device.h k_inverse_persist): two LDS regions of N + right halo
-  // (rounded to whole 64-vector DMA instructions), rows by LDS-DMA, the resident grid walks the batch.
-  // Contract: PERIODIC sequential sums, every detail level and the approximation present, no
-  // thresholds, aligned rows, short unrolled filters, full slabs of whole waves.
-  bool persist = false;
-  int64_t dma_vec = 0;
-  const unsigned all_levels = J >= 32 ? 0xFFFFFFFFu : ((1u << J) - 1u);
-  if (tu.inv_persist && !tu.force_tiled && !pair && boundary == VW_PERIODIC && !approx_zero && !thr &&
-      (detail_mask & all_levels) == all_levels && inv_io && L <= 8 && L <= tu.unroll_max && has_unrolled_taps(L) &&
-      max_hl == 0 && nvec % 64 == 0) {
-    const int pnv = inv_nv2 ? 2 : 4;
-    const int64_t hvec = round_up((max_hr + V - 1) / V, 64);
-    const int64_t th = nvec / pnv;
-    const int64_t bytes = 2 * (nvec + hvec) * V * (int64_t)sizeof(T);
-    if (hvec <= nvec && th % 64 == 0 && th <= (pnv == 2 ? 1024 : 512) && bytes <= kLdsBytes / 2) {
-      persist = true;
-      fused = true;
-      fit = true;
-      db = false;
-      dma_vec = nvec + hvec;
-      nv = pnv;
-      threads = (int)th;
-      lds = (int)bytes;
-    }
-  }
-  if (!persist && !tu.force_tiled) {
+  if (!tu.force_tiled) {
     if (pair || db) fused = fused_plan(tu, N, V, sizeof(T), 2 * region, &threads, &nv, &lds, &fit, inv_nv2);
     if (!fused && !pair) {
       db = false;
@@ -1425,18 +1278,12 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     a.details = details; a.approx = approx; a.y = y; a.B = B; a.N = (int)N; a.J = J;
     a.db = db ? 1 : 0;
     a.hlpad_a = hlpad; a.hlpad_d = hlpad; a.region_d = (int)region;
-    if (persist) {
-      a.persist = 1;
-      a.dma_nt = tu.dma_nt;
-      a.dma_vec = (int)dma_vec;
-      a.region_d = (int)(dma_vec * V);
-    }
     a.vec_io = (N % V == 0) && aligned16(details) && aligned16(approx) && aligned16(y);
     a.unrolled = a.vec_io && fit && L <= tu.unroll_max;
     a.pair = pair; a.approx_zero = approx_zero; a.thr = thr; a.thr_ld = thr_ld; a.soft = soft; a.taps = L;
     a.rev = tu.inv_rev;
     // register-blocked PERIODIC inverse for long filters (vw_device.h k_inverse_blk)
-    if (tu.blk > 0 && L >= tu.blk && nv != 2 && !pair && !db && !persist && boundary == VW_PERIODIC && a.unrolled &&
+    if (tu.blk > 0 && L >= tu.blk && nv != 2 && !pair && !db && boundary == VW_PERIODIC && a.unrolled &&
         (int64_t)threads * nv == nvec) {
       bool okb = true;
       int64_t buf = 0;
@@ -1493,38 +1340,11 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       for (int k = 0; k < groups[j - 1]; ++k) ext += round_up((int64_t)(L - 1) * lv[j - 1 + k].s, V);
       if ((mtile + ext) / V <= (int64_t)kMultiInvNI * 256) start_of[j + groups[j - 1] - 1] = j;
     }
-    // streaming inverse of levels 1..gs (VW_INV_STREAM): replaces the multi-level groups it covers
-    InvStreamArgs<T> isa;
-    memset(&isa, 0, sizeof(isa));
-    int gs = 0;
-    if (tu.inv_stream && !pair && boundary == VW_PERIODIC && !thr && has_unrolled_taps(L) && L <= tu.unroll_max &&
-        aligned16(details) && aligned16(y) && aligned16(approx))
-      gs = inv_stream_plan<T>(lv, J, L, N, B, c->cus, tu.inv_stream, &isa);
-    if (gs >= J) gs = 0;  // (the coarsest approximation must come from a level above: keep it simple)
-    for (int e = 1; gs && e <= J; ++e)
-      if (start_of[e] > 0 && start_of[e] <= gs) start_of[e] = 0;
-    std::vector<char> in_group(J + 1, 0);  // levels inside a multi-level tile group or the stream
+    std::vector<char> in_group(J + 1, 0);  // levels inside a multi-level tile group
     for (int e = 1; e <= J; ++e)
       for (int k = start_of[e]; start_of[e] > 0 && k <= e; ++k) in_group[k] = 1;
-    for (int k = 1; k <= gs; ++k) in_group[k] = 1;
     for (int j = J; j >= 1; --j) {
       T* const nxt = (cur == tmp[0]) ? tmp[1] : tmp[0];  // never the level's own input
-      if (gs && j == gs && cur && aligned16(cur)) {
-        isa.src_a = cur;
-        for (int k = 0; k < gs; ++k) isa.src_d[k] = details + (size_t)k * plane;
-        isa.out = y;
-        isa.taps = L; isa.dma_nt = tu.dma_nt;
-        copy_taps(isa.lo, lo, L);
-        copy_taps(isa.hi, hi, L);
-        int lds = 0;
-        for (int k = 0; k < gs; ++k) lds += isa.cap_a[k] + isa.cap_d[k];
-        lds *= (int)sizeof(T);
-        LaunchTimer lt(c, "inverse_level");
-        hipError_t e = launch_inverse_stream<T>(isa, lds, fma, c->stream);
-        if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse stream launch failed: %s", hipGetErrorString(e));
-        cur = y;
-        break;
-      }
       // streaming deep group with top level j: the lowest jl whose group jl..j fits the LDS budget
       if (!pair && boundary == VW_PERIODIC && !in_group[j] && aligned16(cur) && aligned16(details) &&
           aligned16(y) && deep_plan<T>(tu, lv, j, j, L, N, true, nullptr)) {
@@ -1570,7 +1390,6 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         m.region = (int)round_up(mtile + m.ext[g - 1] + V, V);
         m.vec_io = (N % V == 0) && al;
         m.soft = soft; m.taps = L;
-        m.xcd_chunk = tu.multi_xcd;
         m.rblk = tu.multi_rblk;
         // register prefetch of d_{j-1} while level j computes: whole vectors, every tile of the group
         m.pf = tu.multi_pf && m.vec_io && (int64_t)(mtile + m.ext[g - 1]) / V <= (int64_t)kMultiPF * 256;

@@ -922,36 +922,20 @@ k_forward_persist(const FwdArgs<T> p) {
   long long b = blockIdx.x;
   if (b >= p.B) return;
   int cur = 0;
-  // p.pf_regs: the next signal's row is loaded into registers from level 1 on (a whole signal of time to
-  // land) and written into the free buffer after level J; else it is DMA'd during level J.
-  const bool pfr = p.pf_regs != 0;
-  if (pfr) {
-    T x0[NV][V];
-    load_row_regs<T, NV>(x0, p.x + b * p.ldx, N, nvec, true, false);
-    regs_to_level<T, L, NV>(B0, x0, nvec, N, p.lv[0], p.npow2, (const T*)nullptr);
-  } else {
-    dma_row<T>(B0, p.x + b * p.ldx, nvec, p.dma_nt != 0);
-    wait_vmem();
-  }
+  dma_row<T>(B0, p.x + b * p.ldx, nvec, p.dma_nt != 0);
+  wait_vmem();
   for (;;) {
     T* X = cur ? B1 : B0;
     T* Y = cur ? B0 : B1;
     lds_barrier();  // the row is in X (every wave's share); every read of the previous signal done
-    if (!pfr) {
-      const LevelDesc lv0 = p.lv[0];
-      fill_halo(X, N, lv0.hl, lv0.hr, lv0.mode, p.npow2, (const T*)nullptr, 0);
-    }
+    const LevelDesc lv0 = p.lv[0];
+    fill_halo(X, N, lv0.hl, lv0.hr, lv0.mode, p.npow2, (const T*)nullptr, 0);
     const long long bn = b + G;
     T areg[NV][V];
-    // register prefetch of the next row, issued once per signal outside the level loop (a load under a
-    // per-level condition makes the compiler carry the registers through loop phis and wait vmcnt(0)
-    // at every level); past the last signal it re-reads a valid row that is never used
-    T xreg[NV][V];
-    if (pfr) load_row_regs<T, NV>(xreg, p.x + min(bn, p.B - 1) * p.ldx, N, nvec, true, false);
     for (int j = 1; j <= p.J; ++j) {
       const LevelDesc lv = p.lv[j - 1];
       lds_barrier();  // X = level input + halo; every read of Y (previous level) done
-      if (!pfr && j == p.J && bn < p.B) {
+      if (j == p.J && bn < p.B) {
         dma_row<T>(Y, p.x + bn * p.ldx, nvec, p.dma_nt != 0);  // next signal -> free buffer
       }
       T* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
@@ -963,11 +947,7 @@ k_forward_persist(const FwdArgs<T> p) {
       }
     }
     if (bn >= p.B) break;
-    if (pfr) {
-      regs_to_level<T, L, NV>(Y, xreg, nvec, N, p.lv[0], p.npow2, (const T*)nullptr);  // Y: unused by level J
-    } else {
-      wait_vmcnt<2 * NV>();  // this wave's DMA share landed; level J's stores stay in flight
-    }
+    wait_vmcnt<2 * NV>();  // this wave's DMA share landed; level J's stores stay in flight
     cur = (cur + p.J) & 1;  // the buffer that was free during level J
     b = bn;
   }
@@ -1134,89 +1114,6 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, VW_INV_W)) k_inverse_seq(const
     }
   }
   for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, w * V, N, vec_ok, acc[k]); });
-}
-
-// ---------------------------------------------------------------------------------------------
-// Persistent two-region inverse (PERIODIC K4, sequential sums: MultiLevelMODWTTransform.java:576-589,
-// VectorWaveSwtAdapter.reconstructPeriodic :444-474).  Region Q holds a_j, region P holds d_j, both
-// with their periodic right halo.  The detail rows and each signal's a_J arrive by LDS-DMA
-// (global_load_lds_dwordx4: no VGPRs, so no 16-register prefetch row), each level is
-//   barrier -> approx branch (reads Q) -> wait own DMA of d_j, barrier -> detail branch (reads P)
-//   -> barrier -> DMA d_{j-1} into P, a_{j-1} (registers) into Q with its halo images
-// i.e. three barriers instead of k_inverse_seq's four, and d_{j-1}'s DMA lands while the approximation
-// branch of the next level computes.  The resident grid walks the batch (b = blockIdx.x + k*gridDim.x);
-// during level 1 the next signal's a_J goes into Q as soon as the approximation branch has read it
-// (overlapping the detail branch and the y stores) and its d_J into P after the detail branch, so no
-// signal starts with an exposed row load.  Per output the approximation taps then the detail taps,
-// l ascending: bit-exact in EXACT mode.
-//
-// Host contract (vw_capi.cpp inverse_impl): PERIODIC, every detail level present, approximation
-// present, no thresholds, aligned rows, full slabs (threads * NV == N / V), whole waves, and
-// dma_vec = N / V + right-halo vectors rounded up to 64 (one wave instruction = 64 x 16 B; the halo
-// vectors re-read the row's first vectors, v - N/V).
-// DMA wave-instructions this wave issues for a row of tvec vectors (dma_row_periodic's loop count)
-__device__ __forceinline__ int dma_count(int tvec) {
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6, nc = tvec / 64;
-  return wv < nc ? (nc - wv + nw - 1) / nw : 0;
-}
-
-template <typename T>
-__device__ __forceinline__ int dma_row_periodic(T* buf, const T* __restrict__ src, int nvec, int tvec, bool nt) {
-  constexpr int V = VT<T>::V;
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), nw = blockDim.x >> 6;
-  int n = 0;
-  for (int c = wv; c * 64 < tvec; c += nw, ++n) {  // wave-uniform loop (scalar wv)
-    int v = c * 64 + lane;
-    v = v < nvec ? v : v - nvec;
-    lds_dma16((unsigned)(uintptr_t)(buf + c * 64 * V), src + (size_t)v * V, nt);
-  }
-  return n;
-}
-
-template <typename T, int L, bool FMA, int NV>
-__global__ void __attribute__((amdgpu_flat_work_group_size(1, NV == 2 ? 1024 : 512),
-                               amdgpu_waves_per_eu(NV == 2 ? 8 : 4)))
-k_inverse_persist(const InvArgs<T> p) {
-  constexpr int V = VT<T>::V;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  T* const Q = reinterpret_cast<T*>(smem);               // a_j + halo
-  T* const P = reinterpret_cast<T*>(smem) + p.region_d;  // d_j + halo
-  const int N = p.N;
-  const int nvec = N / V;
-  const int tvec = p.dma_vec;
-  const int J = p.J;
-  const long long G = gridDim.x;
-  const size_t plane = (size_t)p.B * (size_t)N;
-  long long b = blockIdx.x;
-  if (b >= p.B) return;
-  dma_row_periodic<T>(Q, p.approx + b * (size_t)N, nvec, tvec, p.dma_nt != 0);
-  dma_row_periodic<T>(P, p.details + (size_t)(J - 1) * plane + b * (size_t)N, nvec, tvec, p.dma_nt != 0);
-  wait_vmcnt_rt(dma_count(tvec));  // a_J landed (d_J may still be in flight)
-  for (;;) {
-    const long long bn = b + G;
-    T acc[NV][V];
-    for (int j = J; j >= 1; --j) {
-      const LevelDesc lv = p.lv[j - 1];
-      lds_barrier();  // Q = a_j + halo; every read of the previous level done
-      zero_regs<T, NV>(acc);
-      inv_row<T, L, FMA, NV>(Q, nvec, lv.s, lv.dir_a, lv.off_a, p.lo, p.taps, acc);
-      wait_vmem();    // this wave's share of d_j (the only vector-memory operations in flight but stores)
-      lds_barrier();  // P = d_j + halo; every read of Q done
-      if (j == 1 && bn < p.B) dma_row_periodic<T>(Q, p.approx + bn * (size_t)N, nvec, tvec, p.dma_nt != 0);  // next a_J
-      inv_row<T, L, FMA, NV>(P, nvec, lv.s, lv.dir_d, lv.off_d, p.hi, p.taps, acc);
-      if (j > 1) {
-        lds_barrier();  // every read of P done
-        dma_row_periodic<T>(P, p.details + (size_t)(j - 2) * plane + b * (size_t)N, nvec, tvec, p.dma_nt != 0);
-        regs_to_level<T, L, NV>(Q, acc, nvec, N, p.lv[j - 2], 0, (const T*)nullptr);
-      }
-    }
-    for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, w * V, N, true, acc[k]); });
-    if (bn >= p.B) break;
-    lds_barrier();  // every read of P (level 1's detail branch) done
-    const int nd = dma_row_periodic<T>(P, p.details + (size_t)(J - 1) * plane + bn * (size_t)N, nvec, tvec, p.dma_nt != 0);
-    wait_vmcnt_rt(NV + nd);  // the next a_J landed; the y stores and the d_J DMA stay in flight
-    b = bn;
-  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2242,291 +2139,6 @@ __global__ void __launch_bounds__(12 * R) k_inverse_sweep3(const LevelArgs<T> p)
 }
 
 // ---------------------------------------------------------------------------------------------
-// Streaming multi-level forward for long PERIODIC signals (BatchStreamingMODWT's 2^20-sample blocks:
-// BatchStreamingMODWT.java:110-158 -> BatchSIMDMODWT.batchMultiLevelMODWTSoA :343-424; the cascade of
-// MultiLevelMODWTTransform.decompose :243-251 with ScalarOps.circularConvolveMODWT :700-723 per level).
-//
-// One workgroup streams one segment of one signal, left to right, in chunks of C = 1024 vectors.  Level
-// k of the group keeps its INPUT in an LDS ring: the last H_k = (L-1)*s_k samples (what the next chunk
-// still reads) plus the chunk being produced.  Per chunk every level runs once -- read its ring, write
-// d_k to HBM and its approximation into ring k+1 (the last level's to HBM) -- so x is read once, each
-// output written once, nothing is recomputed (the multi-level tiles re-read and re-compute their reach,
-// the per-level sweeps round-trip every approximation through HBM).  The input chunk c+1 arrives by
-// LDS-DMA into ring 0 while levels 2..g of chunk c compute.
-//
-// Periodic boundary: the stream starts `warm` samples before the segment (positions mod N).  Level k's
-// outputs depend on its inputs back to sum_{m<=k} H_m samples; from stream position warm >= sum H on,
-// every ring holds exactly the values the reference's (t - l) mod N would read, so the stored outputs
-// are the reference's (the warm-up ones, computed from not-yet-valid ring slots, are never stored).
-// Per output both filters from one read per tap, taps ascending: bit-exact in EXACT mode.
-//
-// Thread t owns vector t of every chunk (samples u = t*V .. t*V+V-1).  A ring slot is the stream
-// position mod the ring's capacity; a chunk's base slot per ring is workgroup-uniform, each read wraps
-// with two selects (the history reaches back up to H_k, the chunk forward up to C).
-template <typename T>
-__device__ __forceinline__ int ring_slot(int sl, int cap) {
-  sl += sl < 0 ? cap : 0;
-  return sl - (sl >= cap ? cap : 0);
-}
-
-template <typename T, int L, bool FMA, int S>
-__device__ __forceinline__ void stream_window(const T* ring, int cap, int base, const T* lo, const T* hi,
-                                              T (&al)[VT<T>::V], T (&ah)[VT<T>::V]) {
-  // S = 1 / 2: a register window of aligned vectors (fwd_window's chunks), each vector's slot wrapped
-  constexpr int V = VT<T>::V;
-  using vec = typename VT<T>::v;
-  static_for<0, (L + kWinTaps - 1) / kWinTaps>([&](auto c) __attribute__((always_inline)) {
-    constexpr int I0 = decltype(c)::value * kWinTaps;
-    constexpr int I1 = (I0 + kWinTaps < L) ? I0 + kWinTaps : L;
-    constexpr int A = floor_div(-(I1 - 1) * S, V) * V;
-    constexpr int E = (floor_div(V - 1 - I0 * S, V) + 1) * V;
-    constexpr int NE = E - A;
-    T w[NE];
-#pragma unroll
-    for (int k = 0; k < NE / V; ++k) {
-      const vec v = *reinterpret_cast<const vec*>(ring + ring_slot<T>(base + A + k * V, cap));
-#pragma unroll
-      for (int e = 0; e < V; ++e) w[k * V + e] = v[e];
-    }
-#pragma unroll
-    for (int i = I0; i < I1; ++i) {
-      vmadd<FMA, kPkFwd>(al, &w[-i * S - A], lo[i]);
-      vmadd<FMA, kPkFwd>(ah, &w[-i * S - A], hi[i]);
-    }
-  });
-}
-
-template <typename T, int L, bool FMA>
-__device__ __forceinline__ void stream_level(const T* ring, int cap, int base, int s, const T* lo, const T* hi,
-                                             T (&al)[VT<T>::V], T (&ah)[VT<T>::V]) {
-  constexpr int V = VT<T>::V;
-  using vec = typename VT<T>::v;
-#pragma unroll
-  for (int e = 0; e < V; ++e) { al[e] = T(0); ah[e] = T(0); }
-  if (s == 1) return stream_window<T, L, FMA, 1>(ring, cap, base, lo, hi, al, ah);
-  if constexpr (V == 4) {
-    if (s == 2) return stream_window<T, L, FMA, 2>(ring, cap, base, lo, hi, al, ah);
-  }
-#pragma unroll
-  for (int i = 0; i < L; ++i) {  // s a multiple of V: aligned 16-byte reads
-    const vec v = *reinterpret_cast<const vec*>(ring + ring_slot<T>(base - i * s, cap));
-    vmadd<FMA, kPkFwd>(al, v, lo[i]);
-    vmadd<FMA, kPkFwd>(ah, v, hi[i]);
-    if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // <= 4 reads in flight
-  }
-}
-
-template <typename T, int L, bool FMA>
-__global__ void __launch_bounds__(kStreamThreads) k_forward_stream(const StreamArgs<T> p) {
-  constexpr int V = VT<T>::V;
-  constexpr int C = kStreamThreads * V;  // samples per chunk
-  using vec = typename VT<T>::v;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  T* const lds = reinterpret_cast<T*>(smem);
-  const long long b = blockIdx.x / p.seg;
-  const int sg = blockIdx.x % p.seg;
-  if (b >= p.B) return;
-  const int N = p.N;
-  const int u = threadIdx.x * V;                     // this thread's samples within a chunk
-  const int q0 = sg * p.seglen;                      // first stored output of the segment
-  const int nc = (p.warm + p.seglen) / C;            // chunks streamed
-  const int wc = p.warm / C;                         // warm-up chunks (nothing stored)
-  int pos0 = q0 - p.warm;                            // signal position of stream position 0
-  while (pos0 < 0) pos0 += N;
-  const T* __restrict__ src = p.src + b * p.lda;
-  const size_t row = (size_t)b * (size_t)N;
-  const bool nt = p.dma_nt != 0;
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  auto wrapN = [&](int q) { q -= q >= N ? N : 0; return q - (q >= N ? N : 0); };  // q < 3N
-  // chunk c of the input -> ring 0 (one 64-vector DMA instruction per wave: 16 waves x 1 KiB)
-  auto dma_chunk = [&](int c, int cbase) {  // cbase: ring-0 slot of the chunk (a multiple of 64 vectors)
-    int sl = cbase + wv * 64 * V;
-    sl -= sl >= p.cap[0] ? p.cap[0] : 0;
-    const int q = wrapN(pos0 + c * C + (wv * 64 + lane) * V);
-    lds_dma16((unsigned)(uintptr_t)(lds + p.off[0] + sl), src + q, nt);
-  };
-  int base[kMaxGroup];                               // chunk base slot per ring (uniform)
-#pragma unroll
-  for (int k = 0; k < kMaxGroup; ++k) base[k] = 0;
-  dma_chunk(0, 0);
-  wait_vmem();
-  for (int c = 0; c < nc; ++c) {
-    const bool store = c >= wc;
-    const int q = wrapN(pos0 + c * C + u);           // signal position of this thread's first sample
-    for (int k = 0; k < p.g; ++k) {
-      lds_barrier();  // ring k holds the level's input up to this chunk; every read of its slots being
-                      // overwritten below is done
-      if (k == 1 && c + 1 < nc) {                    // ring 0's chunk-c reads are done (level 0 finished)
-        const int nb = base[0] + C;
-        dma_chunk(c + 1, nb - (nb >= p.cap[0] ? p.cap[0] : 0));
-      }
-      const int s = p.s0 << k;
-      T al[V], ah[V];
-      stream_level<T, L, FMA>(lds + p.off[k], p.cap[k], base[k] + u, s, p.lo, p.hi, al, ah);
-      vec oa, od;
-#pragma unroll
-      for (int e = 0; e < V; ++e) { oa[e] = al[e]; od[e] = ah[e]; }
-      if (store) {
-        stream_store<VW_FWD_STORE_AUX, vec>(p.out_d[k] + row, q / V, od);
-        if (k == p.g - 1) stream_store<VW_FWD_STORE_AUX, vec>(p.out + row, q / V, oa);
-      }
-      if (k + 1 < p.g) *reinterpret_cast<vec*>(lds + p.off[k + 1] + ring_slot<T>(base[k + 1] + u, p.cap[k + 1])) = oa;
-    }
-    // the next chunk's base slot in every ring
-#pragma unroll
-    for (int k = 0; k < kMaxGroup; ++k) {
-      if (k < p.g) {
-        int nb = base[k] + C;
-        base[k] = nb - (nb >= p.cap[k] ? p.cap[k] : 0);
-      }
-    }
-    if (c + 1 < nc) wait_vmcnt_rt(store ? p.g : 0);  // this wave's DMA of chunk c+1; the stores stay in flight
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Streaming multi-level inverse for long PERIODIC signals (MultiLevelMODWTTransform.reconstruct
-// :339-349 with the K4 sum of :576-589 per level: all approximation taps, then all detail taps, t + l
-// ascending).  The mirror of k_forward_stream: one workgroup streams one segment of one signal from
-// right to left in chunks of C samples (one vector per thread); the finest g levels run once per chunk,
-// coarsest first.  Level k (level jb + k) reads its approximation input from ring A_k and its detail row
-// from ring D_k at t + i*s_k (right reach H_k = (L-1)*s_k) and writes a_{jb+k-1} into A_{k-1} (level 0:
-// to HBM).  A_{g-1} and every D_k are fed by LDS-DMA one chunk ahead, each issued as soon as the level
-// that reads the ring has finished the current chunk (ring capacity H_k + C suffices); every wave waits
-// for exactly its own DMA of the ring a level needs (counts derived below), then the level's barrier.
-// Chunk c covers positions [T_c, T_c + C), T_c = q0 + seglen + warm - (c+1)*C (mod N); a ring slot is
-// base_c + (t - T_c) mod capacity, base_{c+1} = base_c - C.  The first warm / C chunks lie right of the
-// segment and are not stored (the reach argument of k_forward_stream, mirrored).
-template <typename T, int L, bool FMA, int S>
-__device__ __forceinline__ void stream_inv_window(const T* ring, int cap, int base, const T* f, T (&acc)[VT<T>::V]) {
-  constexpr int V = VT<T>::V;
-  using vec = typename VT<T>::v;
-  static_for<0, (L + kWinTaps - 1) / kWinTaps>([&](auto c) __attribute__((always_inline)) {
-    constexpr int I0 = decltype(c)::value * kWinTaps;
-    constexpr int I1 = (I0 + kWinTaps < L) ? I0 + kWinTaps : L;
-    constexpr int A = floor_div(I0 * S, V) * V;
-    constexpr int E = (floor_div(V - 1 + (I1 - 1) * S, V) + 1) * V;
-    constexpr int NE = E - A;
-    T w[NE];
-#pragma unroll
-    for (int k = 0; k < NE / V; ++k) {
-      const vec v = *reinterpret_cast<const vec*>(ring + ring_slot<T>(base + A + k * V, cap));
-#pragma unroll
-      for (int e = 0; e < V; ++e) w[k * V + e] = v[e];
-    }
-#pragma unroll
-    for (int i = I0; i < I1; ++i) vmadd<FMA>(acc, &w[i * S - A], f[i]);
-  });
-}
-
-template <typename T, int L, bool FMA>
-__device__ __forceinline__ void stream_inv_branch(const T* ring, int cap, int base, int s, const T* f,
-                                                  T (&acc)[VT<T>::V]) {
-  constexpr int V = VT<T>::V;
-  using vec = typename VT<T>::v;
-  if (s == 1) {
-    stream_inv_window<T, L, FMA, 1>(ring, cap, base, f, acc);
-  } else if (V == 4 && s == 2) {
-    stream_inv_window<T, L, FMA, 2>(ring, cap, base, f, acc);
-  } else {
-#pragma unroll
-    for (int i = 0; i < L; ++i) {  // s a multiple of V: aligned 16-byte reads
-      const vec v = *reinterpret_cast<const vec*>(ring + ring_slot<T>(base + i * s, cap));
-      vmadd<FMA>(acc, v, f[i]);
-      if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-    }
-  }
-#pragma unroll
-  for (int e = 0; e < V; ++e) asm volatile("" : "+v"(acc[e]));  // the branch's sum completes here
-}
-
-template <typename T, int L, bool FMA>
-__global__ void __launch_bounds__(1024) k_inverse_stream(const InvStreamArgs<T> p) {
-  constexpr int V = VT<T>::V;
-  using vec = typename VT<T>::v;
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  T* const lds = reinterpret_cast<T*>(smem);
-  const long long b = blockIdx.x / p.seg;
-  const int sg = blockIdx.x % p.seg;
-  if (b >= p.B) return;
-  const int N = p.N, C = p.C, g = p.g;
-  const int u = threadIdx.x * V;
-  const int nc = (p.warm + p.seglen) / C;
-  const int wc = p.warm / C;
-  const size_t row = (size_t)b * (size_t)N;
-  const bool nt = p.dma_nt != 0;
-  const int lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  auto wrapN = [&](int q) { return q - (q >= N ? N : 0); };  // q < 2N
-  // one DMA instruction per wave: this wave's 64 vectors of chunk (Tc, base) of a row into a ring
-  auto dma = [&](int ring_off, int cap, int base, const T* __restrict__ src, int Tc) {
-    int sl = base + wv * 64 * V;
-    sl -= sl >= cap ? cap : 0;
-    lds_dma16((unsigned)(uintptr_t)(lds + ring_off + sl), src + row + wrapN(Tc + (wv * 64 + lane) * V), nt);
-  };
-  int T0 = (int)(((long long)sg * p.seglen + p.seglen + p.warm - C) % N);  // T_0
-  int ba[kMaxGroup], bd[kMaxGroup];
-#pragma unroll
-  for (int k = 0; k < kMaxGroup; ++k) { ba[k] = 0; bd[k] = 0; }
-  auto next_base = [&](int bs, int cap) { bs -= C; return bs + (bs < 0 ? cap : 0); };
-  // prologue: chunk 0 of every DMA-fed ring
-  dma(p.off_a[g - 1], p.cap_a[g - 1], 0, p.src_a, T0);
-  for (int k = 0; k < g; ++k) dma(p.off_d[k], p.cap_d[k], 0, p.src_d[k], T0);
-  wait_vmem();
-  int Tc = T0;
-  for (int c = 0; c < nc; ++c) {
-    const bool more = c + 1 < nc;
-    const bool st_prev = c - 1 >= wc;  // chunk c-1 stored y (one store per wave)
-    int Tn = Tc - C;                   // T_{c+1}
-    Tn += Tn < 0 ? N : 0;
-    for (int k = g - 1; k >= 0; --k) {
-      if (c >= 1) {
-        // vector-memory operations this wave issued after the DMA level k needs (see the schedule below)
-        int X;
-        if (k == g - 1) X = g - 2 + (st_prev ? 1 : 0);
-        else if (k >= 1) X = k + (st_prev ? 1 : 0) + ((more && k <= g - 3) ? g - 1 - k : 0);
-        else X = (more && g >= 3) ? g - 1 : 0;
-        wait_vmcnt_rt(X);
-      }
-      lds_barrier();  // A_k / D_k hold chunk c; every read of the ring slots the DMAs below refill is done
-      // schedule: B(g-1): D_0(c) [c >= 1]; B(g-2): A_{g-1}(c+1), D_{g-1}(c+1); B(k <= g-3): D_{k+1}(c+1)
-      if (k == g - 1) {
-        if (c >= 1) dma(p.off_d[0], p.cap_d[0], bd[0], p.src_d[0], Tc);
-      } else if (more) {
-        if (k == g - 2) {
-          dma(p.off_a[g - 1], p.cap_a[g - 1], next_base(ba[g - 1], p.cap_a[g - 1]), p.src_a, Tn);
-          dma(p.off_d[g - 1], p.cap_d[g - 1], next_base(bd[g - 1], p.cap_d[g - 1]), p.src_d[g - 1], Tn);
-        } else {
-          dma(p.off_d[k + 1], p.cap_d[k + 1], next_base(bd[k + 1], p.cap_d[k + 1]), p.src_d[k + 1], Tn);
-        }
-      }
-      const int s = p.s0 << k;
-      T acc[V];
-#pragma unroll
-      for (int e = 0; e < V; ++e) acc[e] = T(0);
-      stream_inv_branch<T, L, FMA>(lds + p.off_a[k], p.cap_a[k], ba[k] + u, s, p.lo, acc);
-      stream_inv_branch<T, L, FMA>(lds + p.off_d[k], p.cap_d[k], bd[k] + u, s, p.hi, acc);
-      vec o;
-#pragma unroll
-      for (int e = 0; e < V; ++e) o[e] = acc[e];
-      if (k > 0) {
-        *reinterpret_cast<vec*>(lds + p.off_a[k - 1] + ring_slot<T>(ba[k - 1] + u, p.cap_a[k - 1])) = o;
-      } else if (c >= wc) {
-        stream_store<VW_INV_STORE_AUX, vec>(p.out + row, wrapN(Tc + u) / V, o);
-      }
-    }
-    for (int k = 0; k < kMaxGroup; ++k) {
-      if (k < g) {
-        ba[k] = next_base(ba[k], p.cap_a[k]);
-        bd[k] = next_base(bd[k], p.cap_d[k]);
-      }
-    }
-    Tc = Tn;
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
 // Multi-level tiles for long PERIODIC signals (host: vw_capi.cpp level_groups).  One workgroup runs
 // a group of consecutive levels over one tile of one signal; the intermediate approximations stay
 // in LDS.  Periodic convolution commutes with shifts, so a level evaluated at a position v outside
@@ -2536,28 +2148,6 @@ __global__ void __launch_bounds__(1024) k_inverse_stream(const InvStreamArgs<T> 
 // (ScalarOps.java:700-723 reads t - l*s), to the right in the inverse (MultiLevelMODWTTransform
 // .java:576-589 reads t + l*s).  The redundant ext/tile of the arithmetic buys one HBM round trip
 // per group instead of one per level.
-// Workgroup -> (signal b, tile t) of the multi-level tile kernels.  xcd_chunk C = 0: the 2-D grid
-// (tiles, signals).  C > 0: a 1-D grid rounded up to 8C; the tiles in signal-major order (u = b * tiles
-// + t) are cut into runs of C neighbours, run k going to the XCD of workgroups k mod 8 (dispatch deals
-// workgroups round-robin over the 8 XCDs: g and g + 8 share one), each XCD taking its runs in order.
-// Neighbouring tiles, whose reaches overlap, then run on one XCD close in time, so the reach a tile
-// re-reads was just brought into that XCD's L2 by its neighbour instead of coming from HBM again.
-// Placement is a speed hint only: any order computes the same outputs.
-__device__ __forceinline__ bool multi_work(int tiles, long long B, int C, long long* b, int* t) {
-  if (C <= 0) {
-    *b = blockIdx.y;
-    *t = blockIdx.x;
-    return true;
-  }
-  const long long id = blockIdx.x;
-  const long long xcd = id & 7, slot = id >> 3;
-  const long long u = ((slot / C) * 8 + xcd) * C + slot % C;
-  if (u >= B * (long long)tiles) return false;
-  *b = u / tiles;
-  *t = (int)(u % tiles);
-  return true;
-}
-
 template <typename T, int L, bool FMA>
 __global__ void __launch_bounds__(256) k_forward_multi(const MultiArgs<T> p) {
   constexpr int V = VT<T>::V;
@@ -2565,11 +2155,9 @@ __global__ void __launch_bounds__(256) k_forward_multi(const MultiArgs<T> p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* X = reinterpret_cast<T*>(smem) + p.ext[0];  // level input, positions [-ext[k], span)
   T* Y = X + p.region;
+  const long long b = blockIdx.y;
   const int N = p.N;
-  long long b;
-  int tix;
-  if (!multi_work((N + p.tile - 1) / p.tile, p.B, p.xcd_chunk, &b, &tix)) return;
-  const int ts = tix * p.tile;
+  const int ts = blockIdx.x * p.tile;
   const int cnt = min(p.tile, N - ts);
   const int span = (cnt + V - 1) / V * V;
   tile_to_lds(X, p.src_a + b * p.lda, N, ts, -p.ext[0], span, kHaloPeriodic, 0, (const T*)nullptr, 0,
@@ -2615,11 +2203,9 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* const A = reinterpret_cast<T*>(smem);  // positions [0, span + ext[k])
   T* const D = A + p.region;
+  const long long b = blockIdx.y;
   const int N = p.N;
-  long long b;
-  int tix;
-  if (!multi_work((N + p.tile - 1) / p.tile, p.B, p.xcd_chunk, &b, &tix)) return;
-  const int ts = tix * p.tile;
+  const int ts = blockIdx.x * p.tile;
   const int cnt = min(p.tile, N - ts);
   const int span = (cnt + V - 1) / V * V;
   const bool vec_ok = p.vec_io != 0;

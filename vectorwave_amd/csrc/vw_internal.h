@@ -56,7 +56,6 @@ struct FwdArgs {
   int vec_io;
   int unrolled;         // 1: the tap-unrolled kernel may run (aligned rows, full slabs; vw_capi fused_plan)
   int dma_nt;           // k_forward_persist: non-temporal LDS-DMA of the signal rows
-  int pf_regs;          // k_forward_persist: next row prefetched into registers from level 1 (not DMA'd at level J)
   int validate;         // 1: non-finite check on input and outputs (atomicMin into *bad)
   int rev;              // 1: workgroup g owns signal B-1-g (walk order, see vw_capi.cpp walk_reverse)
   unsigned long long* bad;
@@ -94,9 +93,6 @@ struct InvArgs {
   int taps;
   int tap_lds;          // k_inverse_blk: element offset of the LDS tap table
   int blk_tight;        // k_inverse_blk: sparse padding (blk_layout)
-  int persist;          // 1: k_inverse_persist (two regions, LDS-DMA rows, resident grid walks the batch)
-  int dma_nt;           // k_inverse_persist: non-temporal LDS-DMA of the rows
-  int dma_vec;          // k_inverse_persist: vectors per DMA'd row incl. the periodic right halo (x64)
   T lo[kMaxTaps];
   T hi[kMaxTaps];
   LevelDesc lv[kMaxLevels];
@@ -164,52 +160,6 @@ struct MultiArgs {
   int rblk;                  // inverse: register-blocked taps where S is a multiple of V
   int pf;                    // inverse: next level's detail tile prefetched into registers
   int pad;                   // inverse: padded LDS layout at the register-blocked levels (needs pf, rblk)
-  int xcd_chunk;             // > 0: 1-D grid, runs of xcd_chunk neighbouring tiles per XCD (multi_work)
-  T lo[kMaxTaps];
-  T hi[kMaxTaps];
-};
-
-// Streaming multi-level forward (PERIODIC, long signals; vw_device.h k_forward_stream): levels j0 ..
-// j0+g-1 of one signal segment in one launch, each level's input kept in an LDS ring (its history of
-// (L-1)*s samples plus one chunk), the input streamed in chunks of 1024 vectors by LDS-DMA.
-constexpr int kStreamThreads = 1024;
-template <typename T>
-struct StreamArgs {
-  const T* src;              // input of level j0 [B][lda]
-  long long lda;
-  T* out_d[kMaxGroup];       // d of level j0+k [B][N]
-  T* out;                    // approximation of level j0+g-1 [B][N]
-  long long B;
-  int N;
-  int g;                     // levels
-  int s0;                    // spacing of level j0
-  int seg, seglen;           // segments per signal, stored outputs per segment (multiple of the chunk)
-  int warm;                  // warm-up samples streamed before each segment (multiple of the chunk)
-  int cap[kMaxGroup];        // ring capacities (elements; ring 0 a multiple of 64 vectors)
-  int off[kMaxGroup];        // ring offsets (elements)
-  int dma_nt;
-  int taps;
-  T lo[kMaxTaps];
-  T hi[kMaxTaps];
-};
-
-// Streaming multi-level inverse (PERIODIC sequential sums; vw_device.h k_inverse_stream): the finest g
-// levels of a long signal in one launch, streamed right to left; per level an LDS ring of its
-// approximation input (the coarsest one DMA-fed, the others written by the level above) and one of its
-// detail row (DMA-fed), each holding the (L-1)*s samples of history plus one chunk.
-template <typename T>
-struct InvStreamArgs {
-  const T* src_a;             // approximation input of level jb+g-1 [B][N]
-  const T* src_d[kMaxGroup];  // d of level jb+k [B][N]
-  T* out;                     // a_{jb-1} (y when jb = 1) [B][N]
-  long long B;
-  int N, g, s0;               // levels, spacing of level jb
-  int C;                      // chunk samples (threads * V)
-  int seg, seglen, warm;      // as StreamArgs; the warm-up lies to the RIGHT of the segment
-  int cap_a[kMaxGroup], off_a[kMaxGroup];
-  int cap_d[kMaxGroup], off_d[kMaxGroup];
-  int dma_nt;
-  int taps;
   T lo[kMaxTaps];
   T hi[kMaxTaps];
 };
@@ -271,10 +221,7 @@ template <typename T>
 hipError_t launch_inverse_sweepg(const LevelArgs<T>& a, int levels, int ka, int R, bool fma, hipStream_t st);
 template <typename T>
 hipError_t launch_forward_multi(const MultiArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
-template <typename T>
-hipError_t launch_forward_stream(const StreamArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
-template <typename T>
-hipError_t launch_inverse_stream(const InvStreamArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
+
 template <typename T>
 hipError_t launch_inverse_multi(const MultiArgs<T>& a, int lds_bytes, bool fma, hipStream_t st);
 template <typename T>

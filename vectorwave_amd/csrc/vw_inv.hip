@@ -21,32 +21,9 @@ static hipError_t run_inverse_fused_nv(const InvArgs<T>& a, int threads, int lds
   return hipGetLastError();
 }
 
-// Persistent two-region inverse (k_inverse_persist): the resident grid (occupancy query, LDS-bound)
-// walks the batch.  Short unrolled filters only (L <= 8, host contract).
-template <typename T, int L, bool FMA, int NV>
-static hipError_t run_inverse_persist(const InvArgs<T>& a, int threads, int lds, hipStream_t st) {
-  auto k = k_inverse_persist<T, L, FMA, NV>;
-  static LdsOnce configured;
-  hipError_t e = set_lds(k, lds, &configured);
-  if (e != hipSuccess) return e;
-  int dev = 0, cus = 0, per_cu = 0;
-  if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-  if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-  if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, threads, lds)) != hipSuccess) return e;
-  if (per_cu < 1) return hipErrorInvalidConfiguration;
-  const long long grid = std::min<long long>(a.B, (long long)per_cu * cus);
-  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(threads), lds, st, a);
-  return hipGetLastError();
-}
-
 template <typename T, int L, bool FMA>
 static hipError_t run_inverse_fused(const InvArgs<T>& a, int threads, int lds, int nv, hipStream_t st) {
-  if constexpr (L > 0 && L <= 8) {
-    if (a.persist) {
-      return nv == 2 ? run_inverse_persist<T, L, FMA, 2>(a, threads, lds, st)
-                     : run_inverse_persist<T, L, FMA, 4>(a, threads, lds, st);
-    }
-    // NV = 2 (1024 threads): short filters at small batches (host policy)
+  if constexpr (L > 0 && L <= 8) {  // NV = 2 (1024 threads): short filters at small batches (host policy)
     if (nv == 2) return run_inverse_fused_nv<T, L, FMA, 2>(a, threads, lds, st);
   }
   return nv <= 4 ? run_inverse_fused_nv<T, L, FMA, 4>(a, threads, lds, st) : run_inverse_fused_nv<T, L, FMA, 8>(a, threads, lds, st);
