@@ -380,8 +380,12 @@ __device__ __forceinline__ void for_vecs(int nvec, F&& fn) {
 #ifndef VW_LOAD_AUX
 #define VW_LOAD_AUX -1
 #endif
+// Forward coefficient rows (read next by an inverse): sc1.  Same box, alternating, rotated buffer
+// sets (profiles/r04/ab_store_policy_*.log): db4 4096 x 4096 42.8-44.0K (nt) -> 45.1-46.0K Msamples/s,
+// 512 rows 41.0-41.6K -> 42.9-44.1K; write-back (aux 0) 45.1-45.6K / 40.6-41.1K; sym8 / db8 / coif5
+// unchanged (their forwards store through k_forward_blk's write-back path or the tiled kernels).
 #ifndef VW_FWD_STORE_AUX
-#define VW_FWD_STORE_AUX VW_STORE_AUX  // forward coefficient rows (read next by an inverse)
+#define VW_FWD_STORE_AUX 16
 #endif
 #ifndef VW_BLK_NT_M
 #define VW_BLK_NT_M 8  // k_forward_blk: vector strides m below this store write-back (see there)
