@@ -1044,8 +1044,9 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
         if (lv[j].mode != kHaloPeriodic) okb = false;
         hlv = std::max<int>(hlv, (int)(((int64_t)(L - 1) * lv[j].s + V - 1) / V));
       }
-      // the NV = 8 kernel reads at wave-uniform offsets when the halo is whole pad groups (16 vectors)
-      if (nv >= 8 && round_up(hlv, 16) <= nvec) hlv = (int)round_up(hlv, 16);
+      // the kernel reads at wave-uniform (NV = 8) or compile-time (NV = 4) offsets when the halo is whole
+      // pad groups (16 vectors)
+      if (round_up(hlv, 16) <= nvec) hlv = (int)round_up(hlv, 16);
       const int mJ = std::max(1, lv[J - 1].s / V);
       if (nvec % ((int64_t)nv * mJ) != 0 || hlv > nvec) okb = false;
       auto buf_of = [&](int tight) {

@@ -695,7 +695,10 @@ __device__ __forceinline__ void zero_regs(T (&r)[NV][VT<T>::V]) {
 // W waves, longer filters 4 (128 VGPRs; with 512-thread workgroups 5 waves would not add one).
 // NV = 2 (small batches: one 1024-thread workgroup per signal, two per CU = 8 waves per SIMD, 64 VGPRs):
 // twice the waves per signal where the batch leaves the CUs short of signals.
-#define VW_FUSED_W(L, W) ((L) <= 8 ? (W) : 4)
+#ifndef VW_LONG_WAVES
+#define VW_LONG_WAVES 4  // waves per SIMD the fused kernels of long filters (L > 8) are compiled for
+#endif
+#define VW_FUSED_W(L, W) ((L) <= 8 ? (W) : VW_LONG_WAVES)
 #define VW_FUSED_BOUNDS(NV, W)                                                        \
   __attribute__((amdgpu_flat_work_group_size(1, ((NV) <= 4 && (NV) != 2) ? 512 : 1024), \
                  amdgpu_waves_per_eu((NV) == 2 ? 8 : (NV) <= 4 ? (W) : 4)))
@@ -1409,6 +1412,88 @@ __device__ __forceinline__ void blk_fwd_s(const T* Xb, int m, int sh, int pad, c
     }
 }
 
+#ifndef VW_INV_KTAPS
+#define VW_INV_KTAPS 0  // k_inverse_blk: taps from the kernel arguments (SGPRs) instead of LDS
+#endif
+
+#ifndef VW_FWD_KTAPS
+#define VW_FWD_KTAPS 0  // k_forward_blk: taps from the kernel arguments (SGPRs) instead of LDS
+#endif
+
+#ifndef VW_BLK_FWD_C
+#define VW_BLK_FWD_C 1  // NV < 8 forward: compile-time stride forms (0: per-lane blk_phys per read)
+#endif
+
+// blk_fwd at a compile-time stride M (NV < 8, as blk_inv_branch_c): with the halo HLV a multiple of 16
+// vectors (host) the physical offset of logical vector vb + HLV + q*M from vb + HLV's is BlkC::off(q)
+// for every thread.  The reads run q = -(L-1) .. NV-1; they are addressed from the lowest one (Xq), so
+// every offset is a non-negative constant -- an immediate of the ds_read, no per-read address math.
+template <typename T, int L, bool FMA, int NV, int M>
+__device__ __forceinline__ void blk_fwd_c(const T* Xb, const T* flo, const T* fhi, T (&al)[NV][VT<T>::V],
+                                          T (&ah)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  using C = BlkC<M, NV, 0>;
+  constexpr int TC = blk_chunk<T, NV>();
+  constexpr int QMIN = -(L - 1);
+  const T* const Xq = Xb + C::off(QMIN) * V;
+#pragma unroll
+  for (int r = 0; r < NV; ++r)
+#pragma unroll
+    for (int e = 0; e < V; ++e) { al[r][e] = T(0); ah[r][e] = T(0); }
+  static_for<0, (L + TC - 1) / TC>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * TC;
+    constexpr int I1 = (I0 + TC < L) ? I0 + TC : L;
+    T fl[I1 - I0], fh[I1 - I0];
+#pragma unroll
+    for (int i = I0; i < I1; ++i) { fl[i - I0] = flo[i]; fh[i - I0] = fhi[i]; }
+#pragma unroll
+    for (int q = NV - 1 - I0; q > -I1; --q) {
+      const vec x = *reinterpret_cast<const vec*>(Xq + (C::off(q) - C::off(QMIN)) * V);
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        const int i = r - q;
+        if (i >= I0 && i < I1) {
+          vmadd<FMA, kPkFwd>(al[r], x, fl[i - I0]);
+          vmadd<FMA, kPkFwd>(ah[r], x, fh[i - I0]);
+        }
+      }
+      if (((NV - 1 - I0 - q) & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+#pragma unroll
+  for (int r = 0; r < NV; ++r)
+#pragma unroll
+    for (int e = 0; e < V; ++e) {
+      asm volatile("" : "+v"(al[r][e]));
+      asm volatile("" : "+v"(ah[r][e]));
+    }
+}
+
+// One forward level at vector stride m >= 1, NV < 8: the compile-time forms for m = 1..64, the generic one
+// otherwise.  Same reads, same sums (bit-identical to blk_fwd).
+template <typename T, int L, bool FMA, int NV>
+__device__ __forceinline__ void blk_fwd_any(const T* X, const BlkLayout& lo, int HLV, int vb, int m, const T* flo,
+                                            const T* fhi, T (&al)[NV][VT<T>::V], T (&ah)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  const T* Xb = X + blk_phys(lo, vb + HLV) * V;
+  auto go = [&](auto mc) __attribute__((always_inline)) {
+    constexpr int M = decltype(mc)::value;
+    if constexpr (BlkC<M, NV, 0>::ok) blk_fwd_c<T, L, FMA, NV, M>(Xb, flo, fhi, al, ah);
+    else blk_fwd<T, L, FMA, NV>(X, lo, HLV, vb, m, flo, fhi, al, ah);
+  };
+  switch (m) {
+    case 1: go(std::integral_constant<int, 1>{}); break;
+    case 2: go(std::integral_constant<int, 2>{}); break;
+    case 4: go(std::integral_constant<int, 4>{}); break;
+    case 8: go(std::integral_constant<int, 8>{}); break;
+    case 16: go(std::integral_constant<int, 16>{}); break;
+    case 32: go(std::integral_constant<int, 32>{}); break;
+    case 64: go(std::integral_constant<int, 64>{}); break;
+    default: blk_fwd<T, L, FMA, NV>(X, lo, HLV, vb, m, flo, fhi, al, ah); break;
+  }
+}
+
 // Forward, PERIODIC, one signal per workgroup: MultiLevelMODWTTransform.decompose (:243-251) /
 // BatchSIMDMODWT.batchMultiLevelMODWTSoA (:362-377) / VectorWaveSwtAdapter forward.  Level inputs in
 // one LDS buffer (p.region1 == 0: two barriers per level) or two (one barrier).  Left wrap images:
@@ -1427,8 +1512,13 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
   // all 2L taps of a long filter held in registers across it spill (60 for coif5)
   T* const taps = reinterpret_cast<T*>(smem) + p.tap_lds;
   for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) taps[i] = i < L ? p.lo[i] : p.hi[i - L];
+#if VW_FWD_KTAPS
+  const T* const flo = p.lo;  // kernel arguments: scalar loads, SGPR operands
+  const T* const fhi = p.hi;
+#else
   const T* const flo = taps;
   const T* const fhi = taps + L;
+#endif
   const int N = p.N;
   const int nvec = N / V;
   const int NT = blockDim.x;
@@ -1469,7 +1559,15 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
       vb = blk_base<NV>(m);
       const BlkLayout lo = blk_layout(m, NV, p.blk_tight);
       const int sh = __builtin_amdgcn_readfirstlane(lo.sh), pad = __builtin_amdgcn_readfirstlane(lo.pad);
-      if (VW_BLK_SOFF && NV >= 8 && (pad == 0 || (((m * NV) & ((1 << sh) - 1)) == 0 && (HLV & ((1 << sh) - 1)) == 0)))
+      bool fc = false;
+      if constexpr (NV < 8) {
+        if (VW_BLK_FWD_C && (HLV & 15) == 0) {
+          blk_fwd_any<T, L, FMA, NV>(X, lo, HLV, vb, m, flo, fhi, al, ah);
+          fc = true;
+        }
+      }
+      if (fc) {
+      } else if (VW_BLK_SOFF && NV >= 8 && (pad == 0 || (((m * NV) & ((1 << sh) - 1)) == 0 && (HLV & ((1 << sh) - 1)) == 0)))
         blk_fwd_s<T, L, FMA, NV>(X + blk_phys(lo, vb + HLV) * V, m, sh, pad, flo, fhi, al, ah);
       else
         blk_fwd<T, L, FMA, NV>(X, lo, HLV, vb, m, flo, fhi, al, ah);
@@ -1538,8 +1636,14 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_blk(const InvArg
   const int tid = threadIdx.x;
   T* const taps = reinterpret_cast<T*>(smem) + p.tap_lds;  // as k_forward_blk
   for (int i = tid; i < 2 * L; i += NT) taps[i] = i < L ? p.lo[i] : p.hi[i - L];
+#if VW_INV_KTAPS
+  // taps read from the kernel arguments (scalar loads into SGPRs, FMA operands straight from there)
+  const T* const flo = p.lo;
+  const T* const fhi = p.hi;
+#else
   const T* const flo = taps;
   const T* const fhi = taps + L;
+#endif
   auto thr_of = [&](int j) { return p.thr ? load_uniform(p.thr + (size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b) : T(0); };
   const size_t plane = (size_t)p.B * (size_t)N;
   auto m_of = [&](int j) { return p.lv[j - 1].s / V; };
