@@ -1413,11 +1413,11 @@ __device__ __forceinline__ void blk_fwd_s(const T* Xb, int m, int sh, int pad, c
 }
 
 #ifndef VW_INV_KTAPS
-#define VW_INV_KTAPS 0  // k_inverse_blk: taps from the kernel arguments (SGPRs) instead of LDS
+#define VW_INV_KTAPS -1  // k_inverse_blk: taps from the kernel arguments (SGPRs) instead of LDS; -1: at NV >= 8
 #endif
 
 #ifndef VW_FWD_KTAPS
-#define VW_FWD_KTAPS 0  // k_forward_blk: taps from the kernel arguments (SGPRs) instead of LDS
+#define VW_FWD_KTAPS 0  // k_forward_blk: taps from the kernel arguments (SGPRs) instead of LDS (coif5: neutral)
 #endif
 
 #ifndef VW_BLK_FWD_C
@@ -1636,14 +1636,14 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_blk(const InvArg
   const int tid = threadIdx.x;
   T* const taps = reinterpret_cast<T*>(smem) + p.tap_lds;  // as k_forward_blk
   for (int i = tid; i < 2 * L; i += NT) taps[i] = i < L ? p.lo[i] : p.hi[i - L];
-#if VW_INV_KTAPS
-  // taps read from the kernel arguments (scalar loads into SGPRs, FMA operands straight from there)
-  const T* const flo = p.lo;
-  const T* const fhi = p.hi;
-#else
-  const T* const flo = taps;
-  const T* const fhi = taps + L;
-#endif
+  // NV = 8 (sym8 fp64 at N = 16384): the taps from the kernel arguments -- scalar loads, SGPR operands of the
+  // FMAs -- free the VGPRs that held them (128 + 12-40 B/lane of scratch -> 123-125, none) and the LDS tap
+  // reads: inverse 6.72-6.77 -> 6.27-6.32 ms.  NV = 4 (coif5 fp32) keeps them in LDS: there the freed VGPRs
+  // admit a third workgroup per CU and the inverse slows, 6.73-6.80 -> 6.94-6.96 ms
+  // (profiles/r04/ab_ktaps_coif5_sym8.log)
+  constexpr bool ktaps = VW_INV_KTAPS < 0 ? NV >= 8 : VW_INV_KTAPS != 0;
+  const T* const flo = ktaps ? p.lo : taps;
+  const T* const fhi = ktaps ? p.hi : taps + L;
   auto thr_of = [&](int j) { return p.thr ? load_uniform(p.thr + (size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b) : T(0); };
   const size_t plane = (size_t)p.B * (size_t)N;
   auto m_of = [&](int j) { return p.lv[j - 1].s / V; };
