@@ -102,7 +102,7 @@ struct Tuning {
   int sweep2_uc = 2048;        // VW_SWEEP2_UC: u positions per workgroup chunk (512 / 1024 / 2048: 9.68 / 9.50 / 9.33 ms db8 inverse)
   int sweep2_r = 0;            // VW_SWEEP2_R=32: 32-residue groups even where h allows 64 (0 = widest)
   int sweep2_minb = 64;        // VW_SWEEP2_MINB: blocks a residue class needs for the chained sweeps
-  int blk_fwd8 = 0;            // VW_BLK_FWD8=1: register-blocked forward at NV = 8 (1024-thread workgroups)
+  int blk_fwd8 = 1;            // VW_BLK_FWD8=0: fused forward instead of the register-blocked one at NV = 8
 };
 
 // One switch of the Tuning struct by its environment name; value < 0 = the default.  Returns false
@@ -1033,9 +1033,9 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     const bool persist = dbl && a.unrolled && persist_ok(threads, nv, fit);
     // register-blocked PERIODIC forward for long filters (vw_device.h k_forward_blk): padded layouts
     int blk_lds = 0;
-    // (NV = 8: 1024-thread workgroups cap a lane at 128 VGPRs; without spills since round 3, but still
-    // measured slower at sym8 N = 16384 (forward 5.38-5.42 vs 5.15-5.24 ms, profiles/r03/ab_blk_fwd8_sym8.log):
-    // the one-vector-per-tap kernel runs unless VW_BLK_FWD8=1)
+    // (NV = 8, 1024-thread workgroups: with its taps from the kernel arguments (round 4, 99 VGPRs, no
+    // spills) the blocked forward beats the fused one at sym8 N = 16384: 5.27-5.29 -> 4.76 ms,
+    // profiles/r04/ab_blk_fwd8_ktaps_sym8.log; VW_BLK_FWD8=0 restores the fused kernel)
     if (tu.blk > 0 && L >= tu.blk && a.unrolled && !validate && !hist && (int64_t)threads * nv == nvec &&
         (nv == 4 || (nv == 8 && tu.blk_fwd8))) {
       bool okb = true;

@@ -1417,7 +1417,7 @@ __device__ __forceinline__ void blk_fwd_s(const T* Xb, int m, int sh, int pad, c
 #endif
 
 #ifndef VW_FWD_KTAPS
-#define VW_FWD_KTAPS 0  // k_forward_blk: taps from the kernel arguments (SGPRs) instead of LDS (coif5: neutral)
+#define VW_FWD_KTAPS -1  // k_forward_blk: taps from the kernel arguments (SGPRs) instead of LDS; -1: at NV >= 8 (coif5 NV = 4: neutral)
 #endif
 
 #ifndef VW_BLK_FWD_C
@@ -1512,13 +1512,11 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
   // all 2L taps of a long filter held in registers across it spill (60 for coif5)
   T* const taps = reinterpret_cast<T*>(smem) + p.tap_lds;
   for (int i = threadIdx.x; i < 2 * L; i += blockDim.x) taps[i] = i < L ? p.lo[i] : p.hi[i - L];
-#if VW_FWD_KTAPS
-  const T* const flo = p.lo;  // kernel arguments: scalar loads, SGPR operands
-  const T* const fhi = p.hi;
-#else
-  const T* const flo = taps;
-  const T* const fhi = taps + L;
-#endif
+  // kernel-argument taps (scalar loads, SGPR operands) at NV = 8 as in k_inverse_blk: fp64 L = 16 128 VGPRs
+  // + 12 B/lane of scratch -> 99, none
+  constexpr bool ktaps = VW_FWD_KTAPS < 0 ? NV >= 8 : VW_FWD_KTAPS != 0;
+  const T* const flo = ktaps ? p.lo : taps;
+  const T* const fhi = ktaps ? p.hi : taps + L;
   const int N = p.N;
   const int nvec = N / V;
   const int NT = blockDim.x;
