@@ -728,9 +728,11 @@ def run(args, world, rank, local):
     # headline: 512 rows) the passes are short and each leaves the GPU half idle at its ends, so overlapping
     # consecutive steps wins (37.7-38.0K -> 42.1-42.4K) while splitting the rows over two contexts loses
     # (34.9-35.2K); from 1024 rows on two contexts win (42.3K vs 37.3-37.5K at 1024, 42.2-44.2K vs 40.0-40.6K
-    # at 4096).
+    # at 4096).  Only for signals the one-workgroup-per-signal kernels hold (N <= 16384): the long-signal
+    # kernels tile every signal over many workgroups, and db8-stream (256 x 2^20) runs 15.1-15.3K
+    # sequentially vs 14.7-14.8K overlapped (profiles/r04/ab_schedule_db8.log).
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    overlap = pipeline == "fwd+inv" and (args.overlap_steps or (not args.contexts and rows <= 2 * cus))
+    overlap = pipeline == "fwd+inv" and (args.overlap_steps or (not args.contexts and rows <= 2 * cus and N <= 16384))
     if overlap:
         K = 1
         engines, streams = engines[:1], streams[:1]
