@@ -6,6 +6,8 @@
 #   bench:<args>                 one bench.py line into gpurun_out/bench_<n>.json
 #   prof:<args>                  rocprofv3 --kernel-trace --stats of bench.py into gpurun_out/prof_<n>
 #   pmc:<cfg>:<args>             FETCH_SIZE / WRITE_SIZE passes -> gpurun_out/hbm_traffic_<cfg>.json
+#                                (one context: pass --contexts 1; VW_COMMIT=<sha> stamps captured_at)
+#   grp:<args>                   prof:<args>, then the trace grouped per launch shape -> gpurun_out/prof_<n>_groups.txt
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -31,18 +33,24 @@ for s in "$@"; do
       timeout -k 10 300 python bench.py $arg > "gpurun_out/bench_$n.json" 2> "gpurun_out/bench_$n.err"; rc=$?
       tail -c 600 "gpurun_out/bench_$n.json"; echo; echo "[$s] rc=$rc"
       [ $rc -ne 0 ] && { tail -5 "gpurun_out/bench_$n.err"; exit $rc; } ;;
-    prof)
+    prof|grp)
       # shellcheck disable=SC2086
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/prof_$n" -o run -- \
         python3 bench.py --no-cpu-baseline $arg > "gpurun_out/prof_$n.log" 2>&1; rc=$?
-      echo "[$s] rc=$rc"; fatal $rc && exit $rc ;;
+      echo "[$s] rc=$rc"; fatal $rc && exit $rc
+      if [ "$kind" = grp ] && [ $rc -eq 0 ]; then
+        python3 tools/rocprof_groups.py "gpurun_out/prof_$n" --commit "${VW_COMMIT:-}" --cmd "bench.py --no-cpu-baseline $arg" \
+          --min-launches 3 > "gpurun_out/prof_${n}_groups.txt"
+        grep -E "k_(forward|inverse|noise)" "gpurun_out/prof_${n}_groups.txt" || true
+      fi ;;
     pmc)
       cfg="${arg%%:*}"; bargs="${arg#*:}"
       rm -rf gpurun_out/pmc
       PMC_GROUPS="FETCH_SIZE
 WRITE_SIZE" BENCH_ARGS="--config $cfg $bargs" bash tools/pmc.sh; rc=$?
       if [ $rc -eq 0 ]; then
-        python3 tools/hbm_traffic.py gpurun_out/pmc > "gpurun_out/hbm_traffic_$cfg.json"
+        case "$cfg" in db4) rows=4096 ;; sym8-denoise) rows=16384 ;; db8-stream) rows=256 ;; coif5-f32) rows=65536 ;; *) rows=0 ;; esac
+        python3 tools/hbm_traffic.py gpurun_out/pmc --commit "${VW_COMMIT:-}" --rows "$rows" > "gpurun_out/hbm_traffic_$cfg.json"
         python3 tools/pmc_summary.py gpurun_out/pmc > "gpurun_out/pmc_traffic_$cfg.txt"
         cat "gpurun_out/hbm_traffic_$cfg.json"
       fi

@@ -38,28 +38,38 @@ def pass_of(kernel):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root", nargs="?", default="gpurun_out/pmc")
-    ap.add_argument("--passes", type=int, default=0, help="passes per family in the run (0: one per dispatch)")
+    ap.add_argument("--passes", type=int, default=0,
+                    help="passes per family in the run (0: the launch count of the family's least-launched kernel, "
+                         "i.e. every kernel of a pass runs at least once per pass)")
     ap.add_argument("--commit", default="")
+    ap.add_argument("--rows", type=int, default=0, help="signals per pass (bench.py scales by its rank's rows)")
     a = ap.parse_args()
     # counter -> pass -> list of per-dispatch values (one csv row per dispatch and counter)
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     names = collections.defaultdict(set)
+    kcount = collections.defaultdict(collections.Counter)   # pass -> kernel -> FETCH_SIZE rows (dispatches)
     for f in sorted(glob.glob(os.path.join(a.root, "p*", "**", "*counter_collection.csv"), recursive=True)):
         for r in csv.DictReader(open(f)):
             p = pass_of(r["Kernel_Name"])
             if p is None:
                 continue
             vals[p][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            names[p].add(r["Kernel_Name"].split("(")[0].replace("void ", ""))
+            kn = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            names[p].add(kn)
+            if r["Counter_Name"] == "FETCH_SIZE":
+                kcount[p][kn] += 1
     out = {"captured_at": a.commit or None}
+    if a.rows:
+        out["rows"] = a.rows
     for p, cs in vals.items():
         if "FETCH_SIZE" not in cs or "WRITE_SIZE" not in cs:
             continue
-        n = a.passes or len(cs["FETCH_SIZE"])
+        n = a.passes or min(kcount[p].values())
         fetch = 2.0 * 1024.0 * sum(cs["FETCH_SIZE"]) / n
         write = 1024.0 * sum(cs["WRITE_SIZE"]) / n
         out[p] = {"bytes_per_launch": round(fetch + write), "fetch_bytes": round(fetch), "write_bytes": round(write),
                   "dispatches": len(cs["FETCH_SIZE"]), "passes": n, "kernels": sorted(names[p]),
+                  "launches_per_pass": {k: round(c / n, 3) for k, c in sorted(kcount[p].items())},
                   "correction": "FETCH_SIZE x2 (gfx950 wide streaming reads), KiB -> bytes; per pass"}
     json.dump(out, sys.stdout, indent=1)
     print()
