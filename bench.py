@@ -36,7 +36,7 @@ import socket
 import subprocess
 import sys
 import time
-from ctypes import c_void_p
+from ctypes import byref, c_void_p
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -402,80 +402,54 @@ def measure_overlap(torch, dist, world, pt, eng_i, stream_i, flags, steps, warmu
     every forward on the part's context / stream F, every inverse on context I / stream I, step i's
     inverse after its forward (event), step i's forward after step i - R's inverse (the buffer set it
     overwrites), R >= 2 rotated output sets.  So step i + 1's forward overlaps step i's inverse; each
-    step still runs its full forward and inverse.  Direct C-ABI calls on the two streams: the same steps
-    recorded into one graph (torch stream capture over both streams) lost the overlap -- 35.6K vs 42.3K
-    Msamples/s at 512 rows (profiles/r04/ab_overlap_graph.log vs ab_overlap_direct_512.log).  Returns
-    device seconds of the K timed steps (events on stream F around them, stream I joined back)."""
-    nat, lib, w, J, N, B = pt.nat, pt.lib, pt.w, pt.J, pt.N, pt.rows
+    step still runs its full forward and inverse.  The steps are issued by the engine itself
+    (vw_pipeline_run: one C call for all K steps) -- not a Python call per pass, whose
+    ~50 us per step at 512 rows was as long as the GPU step.  Graph capture is no substitute: the same
+    steps recorded into one graph lost the overlap (35.6K vs 42.3K Msamples/s at 512 rows,
+    profiles/r04/ab_overlap_graph.log).  Returns (device s of the K timed steps -- events on stream F
+    around them, stream I joined back --, host wall s of the same interval, host s spent issuing them)."""
+    nat, lib = pt.nat, pt.lib
     R = pt.rotate
     assert R >= 2 and pt.pipeline == "fwd+inv", "overlapped steps need >= 2 buffer sets (outputs too) and fwd+inv"
-    p = lambda t: c_void_p(t.data_ptr())  # noqa: E731
-    fwd = lib.vw_modwt_forward_f32 if pt.f32 else lib.vw_modwt_forward_f64
-    inv = lib.vw_modwt_inverse_f32 if pt.f32 else lib.vw_modwt_inverse_f64
-    ptrs = [(p(st["x"]), p(st["det"]), p(st["app"]), p(st["y"])) for st in pt.sets]
     sF, sI = pt.stream, stream_i
     eF, eI = pt.eng, eng_i
     with torch.cuda.stream(sI):
         eI.bind_torch_stream()
     with torch.cuda.stream(sF):
         eF.bind_torch_stream()
-    # one event pair per buffer set, reused: step i records ev_f[r] / ev_i[r] (r = i mod R); step i + R's
-    # forward waits for ev_i[r] before overwriting set r (host work per step kept small: at 512 rows a
-    # step is ~50 us of GPU time)
-    ev_f = [torch.cuda.Event() for _ in range(R)]
-    ev_i = [torch.cuda.Event() for _ in range(R)]
-    live = [False] * R
-    cx_f, cx_i = eF.ctx, eI.ctx
-    args_f = [(xp, B, N, N, pt.lo_a, pt.hi_a, pt.L, w.wavelet_id, nat.PERIODIC, J, flags, dp, ap)
-              for xp, dp, ap, _ in ptrs]
-    args_i = [(dp, ap, B, N, pt.lo_a, pt.hi_a, pt.L, w.wavelet_id, nat.PERIODIC, J, 0xFFFFFFFF, 0, flags, yp)
-              for _, dp, ap, yp in ptrs]
-
-    def one(i):
-        r = i % R
-        if live[r]:
-            sF.wait_event(ev_i[r])
-        st = fwd(cx_f, *args_f[r])
-        if st:
-            pt._check(st)
-        ev_f[r].record(sF)
-        sI.wait_event(ev_f[r])
-        st = inv(cx_i, *args_i[r])
-        if st:
-            pt._check(st)
-        ev_i[r].record(sI)
-        live[r] = True
-        pt.last = r
-
-    def join():
-        e = torch.cuda.Event()
-        e.record(sI)
-        sF.wait_event(e)
-        for r in range(R):
-            live[r] = False
-
-    n = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < settle_s or n < warmup:
-        one(n)
-        n += 1
-        if n % 20 == 0:
+    arr = lambda key: (c_void_p * R)(*[st[key].data_ptr() for st in pt.sets])  # noqa: E731
+    pipe = c_void_p()
+    pt._check(lib.vw_pipeline_create(eF.ctx, eI.ctx, 4 if pt.f32 else 8, R, arr("x"), arr("det"), arr("app"),
+                                     arr("y"), pt.rows, pt.N, pt.lo_a, pt.hi_a, pt.L, pt.w.wavelet_id, nat.PERIODIC,
+                                     pt.J, flags, byref(pipe)))
+    try:
+        n = 0
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < settle_s or n < warmup:
+            k = 20 if n >= warmup else max(1, min(20, warmup - n))
+            pt._check(lib.vw_pipeline_run(pipe, k))
+            n += k
             torch.cuda.synchronize()
-    join()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    ev0.record(sF)
-    for i in range(steps):
-        one(n + i)
-    join()
-    ev1.record(sF)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    return ev0.elapsed_time(ev1) * 1e-3
+        pt._check(lib.vw_pipeline_join(pipe))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        h0 = time.perf_counter()
+        ev0.record(sF)
+        pt._check(lib.vw_pipeline_run(pipe, steps))
+        h1 = time.perf_counter()
+        pt._check(lib.vw_pipeline_join(pipe))
+        ev1.record(sF)
+        torch.cuda.synchronize()
+        h2 = time.perf_counter()
+        pt.last = int(lib.vw_pipeline_last_set(pipe))
+        if world > 1:
+            dist.barrier()
+    finally:
+        lib.vw_pipeline_destroy(pipe)
+    return ev0.elapsed_time(ev1) * 1e-3, h2 - h0, h1 - h0
 
 
 class Workload:
@@ -496,6 +470,8 @@ class Workload:
         self.rows, self.N, self.J, self.pipeline = rows, N, J, pipeline
         self.f32 = dtype == "f32"
         self.graphs = []
+        self.overlap = None        # (inverse engine, stream) of the overlapped-steps schedule
+        self.host_issue_s = None   # overlapped steps: host seconds spent issuing the K timed steps
 
     def close(self):
         for g in self.graphs:
@@ -521,8 +497,10 @@ def measure(torch, dist, world, wl, flags, mode, steps, warmup, settle_s, events
     """
     if getattr(wl, "overlap", None):
         eng_i, stream_i = wl.overlap
-        el = measure_overlap(torch, dist, world, wl.parts[0], eng_i, stream_i, flags, steps, warmup, settle_s)
-        return (el, el), (settle_s, 0), {}, 0, {}
+        el, host_el, issue = measure_overlap(torch, dist, world, wl.parts[0], eng_i, stream_i, flags, steps, warmup,
+                                             settle_s)
+        wl.host_issue_s = issue
+        return (el, host_el), (settle_s, 0), {}, 0, {}
     parts = wl.parts
     main = torch.cuda.current_stream()
     fns = [pt.step_fn(flags) for pt in parts]
@@ -675,6 +653,53 @@ def settle(torch, run1, seconds):
     return time.perf_counter() - t0, n
 
 
+def plan_schedule(args, rows, N, esz, cus, pipeline):
+    """(contexts K, overlapped steps?, (buffer sets R, outputs rotated?)) for `rows` signals on one GPU.
+
+    Contexts per GPU: K parts of the rows, each on its own context + stream (--contexts; 0 = policy: 2
+    above 2 signals per CU -- measured on MI355X, db4 4096 x 4096: 43.6-44.0K -> 44.7-45.7K; 1024 rows:
+    39.4K -> 44.1K; 512 rows: 37.0K -> 36.1K, profiles/r03/ab_contexts.log).
+
+    Buffer sets: with one set the same 128 MiB input was re-read every step and stayed in
+    the Infinity Cache (the persistent forward's LDS-DMA allocates there, the streaming loads and stores
+    around it are non-temporal): same box, db4 4096 x 4096, forward 0.163-0.164 ms with one set vs
+    0.187-0.197 ms with three (profiles/r04/ab_rotate_4096.log).  So every step reads a fresh input:
+    R * input >= 512 MiB, R >= 2.
+
+    Step schedule: `overlap` pipelines consecutive steps over two contexts (step i+1's forward beside step
+    i's inverse, measure_overlap); otherwise the K contexts split the rows.  Policy (measured on MI355X,
+    db4 J=6, rotated sets; profiles/r04/ab_overlap_direct_512.log, ab_overlap_direct_4096.log,
+    ab_overlap_graph.log): at <= 2 signals per CU (the 8-GPU shard of the headline: 512 rows) the passes
+    are short and each leaves the GPU half idle at its ends, so overlapping consecutive steps wins
+    (37.7-38.0K -> 42.1-42.4K) while splitting the rows over two contexts loses (34.9-35.2K); from 1024
+    rows on two contexts win (42.3K vs 37.3-37.5K at 1024, 42.2-44.2K vs 40.0-40.6K at 4096).  Only for
+    signals the one-workgroup-per-signal kernels hold (N <= 16384): the long-signal kernels tile every
+    signal over many workgroups, and db8-stream (256 x 2^20) runs 15.1-15.3K sequentially vs 14.7-14.8K
+    overlapped (profiles/r04/ab_schedule_db8.log)."""
+    K = args.contexts or (2 if rows > 2 * cus else 1)
+    R = args.rotate or max(2, -(-(512 << 20) // max(rows * N * esz, 1)))
+    rot = (R, bool(args.rotate_outputs or not args.rotate))
+    overlap = pipeline == "fwd+inv" and (args.overlap_steps or (not args.contexts and rows <= 2 * cus and N <= 16384))
+    if overlap:
+        K = 1
+        rot = (max(rot[0], 2), True)
+    return K, overlap, rot
+
+
+def make_engines(vw, torch, dev, local, main, K, overlap):
+    """K contexts (the process-wide one first) with their streams (main first), plus the inverse context
+    and stream of the overlapped-steps schedule.  Extra contexts are closed by close_engines."""
+    engines = [vw.Engine.get(local)] + [vw.Engine(local) for _ in range(K - 1)]
+    streams = [main] + [torch.cuda.Stream(device=dev) for _ in range(K - 1)]
+    ov = (vw.Engine(local), torch.cuda.Stream(device=dev)) if overlap else None
+    return engines, streams, ov
+
+
+def close_engines(engines, ov):
+    for e in engines[1:] + ([ov[0]] if ov else []):
+        e.close()
+
+
 def run(args, world, rank, local):
     import torch
     import torch.distributed as dist
@@ -707,37 +732,9 @@ def run(args, world, rank, local):
 
     # ---- strong scaling (headline): rank r owns rows [start, start + rows) of the global batch
     start, rows = shard_rows(Bg, world, rank)
-    # contexts per GPU: K parts of the rank's rows, each on its own context + stream (--contexts; 0 =
-    # policy: 2 above 2 signals per CU -- measured on MI355X, db4 4096 x 4096: 43.6-44.0K -> 44.7-45.7K;
-    # 1024 rows: 39.4K -> 44.1K; 512 rows: 37.0K -> 36.1K (profiles/r03/ab_contexts.log); at or below that,
-    # overlapped steps (below))
-    K = args.contexts or (2 if rows > 2 * torch.cuda.get_device_properties(dev).multi_processor_count else 1)
-    engines = [vw.Engine.get(local)] + [vw.Engine(local) for _ in range(K - 1)]
-    streams = [main] + [torch.cuda.Stream(device=dev) for _ in range(K - 1)]
-    # Buffer sets: with one set the same 128 MiB input was re-read every step and stayed in
-    # the Infinity Cache (the persistent forward's LDS-DMA allocates there, the streaming loads and stores
-    # around it are non-temporal): same box, db4 4096 x 4096, forward 0.163-0.164 ms with one set vs
-    # 0.187-0.197 ms with three (profiles/r04/ab_rotate_4096.log).  So every step reads a fresh input.
-    x_bytes = rows * N * esz
-    R = args.rotate or max(2, -(-(512 << 20) // max(x_bytes, 1)))
-    rot = (R, bool(args.rotate_outputs or not args.rotate))
-    # Step schedule: `overlap` pipelines consecutive steps over two contexts (step i+1's forward beside step
-    # i's inverse, measure_overlap); otherwise the K contexts above split the rows.
-    # Policy (measured on MI355X, db4 J=6, rotated sets; profiles/r04/ab_overlap_direct_512.log,
-    # ab_overlap_direct_4096.log, ab_overlap_graph.log): at <= 2 signals per CU (the 8-GPU shard of the
-    # headline: 512 rows) the passes are short and each leaves the GPU half idle at its ends, so overlapping
-    # consecutive steps wins (37.7-38.0K -> 42.1-42.4K) while splitting the rows over two contexts loses
-    # (34.9-35.2K); from 1024 rows on two contexts win (42.3K vs 37.3-37.5K at 1024, 42.2-44.2K vs 40.0-40.6K
-    # at 4096).  Only for signals the one-workgroup-per-signal kernels hold (N <= 16384): the long-signal
-    # kernels tile every signal over many workgroups, and db8-stream (256 x 2^20) runs 15.1-15.3K
-    # sequentially vs 14.7-14.8K overlapped (profiles/r04/ab_schedule_db8.log).
     cus = torch.cuda.get_device_properties(dev).multi_processor_count
-    overlap = pipeline == "fwd+inv" and (args.overlap_steps or (not args.contexts and rows <= 2 * cus and N <= 16384))
-    if overlap:
-        K = 1
-        engines, streams = engines[:1], streams[:1]
-        rot = (max(rot[0], 2), True)
-    ov = (vw.Engine(local), torch.cuda.Stream(device=dev)) if overlap else None
+    K, overlap, rot = plan_schedule(args, rows, N, esz, cus, pipeline)
+    engines, streams, ov = make_engines(vw, torch, dev, local, main, K, overlap)
     wl = Workload(engines, streams, w, J, rows, N, dtype, pipeline, start, torch, *rot)
     wl.overlap = ov
     footprint = sum(pt.footprint() for pt in wl.parts)
@@ -827,20 +824,29 @@ def run(args, world, rank, local):
         alt = {"accumulation": acc_name(args.config, bool(aflags & nat.FLAG_FMA)),
                "value": round(Bg * N * args.steps / ael / 1e6, 2),
                "kernels_ms": {k: round(ms / n, 5) for k, (ms, n) in afams.items()}}
+    host_issue = wl.host_issue_s
     wl.close()
     del wl
 
     # ---- weak scaling (N > 1): every rank owns a full per-GPU batch of Bg rows (the N = 1 workload)
     weak = None
     if world > 1 and not args.no_weak:
-        wk = Workload(engines, streams, w, J, Bg, N, dtype, pipeline, rank * Bg, torch, *rot)
-        wk.overlap = ov
+        # the full per-GPU batch gets its own schedule, buffer sets and contexts (reusing the
+        # shard's R and overlap decision allocated 32 rotated 4096 x 4096 sets and overlapped 4096 rows)
+        Kw, overlap_w, rot_w = plan_schedule(args, Bg, N, esz, cus, pipeline)
+        engines_w, streams_w, ov_w = make_engines(vw, torch, dev, local, main, Kw, overlap_w)
+        wk = Workload(engines_w, streams_w, w, J, Bg, N, dtype, pipeline, rank * Bg, torch, *rot_w)
+        wk.overlap = ov_w
         (wel, _), _, _, _, _ = measure(torch, dist, world, wk, flags, args.launch, args.steps, args.warmup,
                                        min(args.settle, 0.3), False)
         wel = max_over_ranks(torch, dist, world, wel, dev)
         weak = {"value": round(world * Bg * N * args.steps / wel / 1e6, 2), "batch_per_gpu": Bg,
                 "ms_per_step": round(wel / args.steps * 1e3, 4), "global_batch": world * Bg}
         wk.close()
+        del wk
+        close_engines(engines_w, ov_w)
+
+    close_engines(engines, ov)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -861,6 +867,11 @@ def run(args, world, rank, local):
             "timing": {"value_from": "HIP events around the K timed steps on each rank's stream, max over ranks",
                        "device_s": round(elapsed, 7), "host_wall_s": round(host_elapsed, 7),
                        "host_wall_value": round(Bg * N * args.steps / host_elapsed / 1e6, 2),
+                       "host_issue_us_per_step": (round(host_issue / args.steps * 1e6, 2) if host_issue is not None
+                                                  else None),
+                       "host_issue_from": ("host clock around the one vw_pipeline_run call that enqueues the K "
+                                           "timed steps (overlapped steps)" if host_issue is not None else
+                                           "graph replay: one launch per context for all K steps"),
                        "collective_inside_timed_region": False},
             "check": checks,
             "higher_is_better": True,
@@ -878,7 +889,8 @@ def run(args, world, rank, local):
                                   "step i's inverse, one buffer set per step in flight)" if overlap else ""),
                 "schedule": "overlap-steps" if overlap else ("contexts" if K > 1 else "sequential"),
                 "contexts_per_gpu": K,
-                "launch": ("direct C-ABI calls on two streams, event edges between them (overlapped steps)"
+                "launch": ("vw_pipeline_run: the engine issues the K steps from C++ on two streams, event edges "
+                           "between them (overlapped steps)"
                            if overlap else LAUNCH_DESC[args.launch]),
                 "buffer_sets": {"sets": rot[0], "outputs_rotated": rot[1], "device_bytes_per_rank": footprint,
                                 "why": "step i works on set i mod R: no step re-reads an input an earlier step left "

@@ -312,6 +312,31 @@ VW_API vw_status vw_capture_end(vw_ctx *ctx, vw_graph **out);
 VW_API vw_status vw_graph_launch(vw_graph *graph, int64_t count);
 VW_API vw_status vw_graph_destroy(vw_graph *graph);
 
+/* ---- pipelined round trips ---------------------------------------------------
+ * A caller that runs forward + inverse over successive batches (a server's per-batch loop over
+ * BatchMODWT.multiLevelAoS then inverseMultiLevelAoS, ext/extensions/modwt/BatchMODWT.java:90-111,
+ * :151-178; the blocks of BatchStreamingMODWT) keeps R >= 2 device buffer sets and lets the engine
+ * issue the steps: step i works on set i mod R, its forward on fwd_ctx's stream, then (event) its
+ * inverse on inv_ctx's stream; step i's forward waits for step i - R's inverse.  Step i + 1's forward
+ * thus overlaps step i's inverse -- what keeps a small batch (<= 2 signals per CU) from leaving the
+ * GPU half idle at each pass's ends -- and the steps are issued from C++, not one host call per pass.
+ * x[r] is [B][N] (ldx = N), details[r] [J][B][N], approx[r] and y[r] [B][N], elements of elem_bytes
+ * (8: f64, 4: f32), all on the contexts' device (both contexts on one device; they may be the same
+ * context, which serialises the steps).  flags: FMA / CORE_LEVELS; SYNC, VALIDATE and HOST_MEMORY are
+ * refused (VW_ERR_ARG).  vw_pipeline_run enqueues `steps` steps and returns; vw_pipeline_join makes
+ * fwd_ctx's stream wait for every enqueued inverse (then the next run starts with no pending edge).
+ * Destroying a context kills its pipelines (run / join then return VW_ERR_STATE). */
+typedef struct vw_pipeline vw_pipeline;
+VW_API vw_status vw_pipeline_create(vw_ctx *fwd_ctx, vw_ctx *inv_ctx, int elem_bytes, int sets, void *const *x,
+                                    void *const *details, void *const *approx, void *const *y, int64_t B,
+                                    int64_t N, const double *lo, const double *hi, int L, int wavelet_id,
+                                    int boundary, int J, unsigned flags, vw_pipeline **out);
+VW_API vw_status vw_pipeline_run(vw_pipeline *p, int64_t steps);
+VW_API vw_status vw_pipeline_join(vw_pipeline *p);
+/* buffer set of the most recently enqueued step (-1 before the first) */
+VW_API int64_t vw_pipeline_last_set(vw_pipeline *p);
+VW_API vw_status vw_pipeline_destroy(vw_pipeline *p);
+
 /* ---- device utilities ---------------------------------------------------- */
 /* x[i] = 2*u - 1 with u = (splitmix64(seed ^ (offset + i)) >> 11) * 2^-53. */
 VW_API vw_status vw_fill_uniform_f64(vw_ctx *ctx, double *x, int64_t count, uint64_t seed, int64_t offset);

@@ -221,3 +221,42 @@ def test_graph_outliving_its_context(engine):
     assert lib.vw_ctx_destroy(ctx) == 0
     assert lib.vw_graph_launch(g, 1) == 10   # VW_ERR_STATE
     assert lib.vw_graph_destroy(g) == 0
+
+
+def test_graph_of_long_centered_median_goes_stale_when_scratch_grows(engine):
+    # the centred median of rows longer than the register path (N > 16384) uses a
+    # per-context scratch; growing it frees the old one, so a graph that recorded the old address must
+    # refuse to replay (VW_ERR_STATE) instead of touching freed memory
+    import torch
+    from ctypes import c_void_p
+    eng = vw.Engine(0)
+    try:
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            eng.bind_torch_stream()
+            lib, ctx = eng.lib, eng.ctx
+            P = lambda t: c_void_p(t.data_ptr())  # noqa: E731
+            x = torch.from_numpy(O.fill_uniform(20000, 42).reshape(1, 20000)).cuda()
+            cen = torch.zeros(1, dtype=torch.float64, device="cuda")
+            out = torch.empty(1, dtype=torch.float64, device="cuda")
+
+            def med():
+                assert lib.vw_median_f64(ctx, P(x), 1, 20000, P(cen), 0, P(out)) == 0, nat.last_error()
+            med()   # sizes the scratch outside the capture
+            torch.cuda.synchronize()
+            ref = float(np.median(np.abs(x.cpu().numpy())))
+            assert out.item() == ref
+            g = eng.capture(med)
+            g.launch(1)
+            torch.cuda.synchronize()
+            assert out.item() == ref
+            big = torch.from_numpy(O.fill_uniform(3 * 40000, 7).reshape(3, 40000)).cuda()
+            cb = torch.zeros(3, dtype=torch.float64, device="cuda")
+            ob = torch.empty(3, dtype=torch.float64, device="cuda")
+            assert lib.vw_median_f64(ctx, P(big), 3, 40000, P(cb), 0, P(ob)) == 0, nat.last_error()
+            torch.cuda.synchronize()
+            assert np.array_equal(ob.cpu().numpy(), np.median(np.abs(big.cpu().numpy()), axis=1))
+            assert lib.vw_graph_launch(g.handle, 1) == 10   # VW_ERR_STATE: the scratch moved
+            g.close()
+    finally:
+        eng.close()

@@ -155,3 +155,17 @@ def test_device_tensors_one_thread_per_context(engine):
                                                 nat.taps_array(w.highPassDecomposition()), 8, w.wavelet_id,
                                                 O.PERIODIC, J, nat.FLAG_HOST_MEMORY, ptrs, ptrs)
         assert st == 7   # VW_ERR_ARG
+        # inverse_device checks every shard before any launch: wrong dtype, mismatched rows,
+        # a different N on one shard, a host tensor -- InvalidArgumentException, nothing enqueued
+        from vectorwave_amd.errors import InvalidArgumentException
+        good = g.forward_device(xs, w, J)
+        bad_cases = [
+            [(good[0][0].float(), good[0][1].float())] + good[1:],
+            [(good[0][0], good[0][1][:-1])] + good[1:],
+            good[:1] + [(good[1][0][..., :-8].contiguous(), good[1][1][..., :-8].contiguous())] + good[2:],
+            good[:2] + [(good[2][0].cpu(), good[2][1].cpu())],
+            [(good[0][0][0], good[0][1])] + good[1:],
+        ]
+        for parts in bad_cases:
+            with pytest.raises(InvalidArgumentException):
+                g.inverse_device(parts, w)

@@ -94,6 +94,13 @@ SIGNATURES = {
     "vw_capture_end": (c_int, [c_void_p, POINTER(c_void_p)]),
     "vw_graph_launch": (c_int, [c_void_p, c_int64]),
     "vw_graph_destroy": (c_int, [c_void_p]),
+    # pipelined round trips: per-set arrays of device pointers (c_void_p * sets)
+    "vw_pipeline_create": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_int64,
+                                   c_int64, _dp, _dp, c_int, c_int, c_int, c_int, c_uint, POINTER(c_void_p)]),
+    "vw_pipeline_run": (c_int, [c_void_p, c_int64]),
+    "vw_pipeline_join": (c_int, [c_void_p]),
+    "vw_pipeline_last_set": (c_int64, [c_void_p]),
+    "vw_pipeline_destroy": (c_int, [c_void_p]),
 }
 
 _lib = None

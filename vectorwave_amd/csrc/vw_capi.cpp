@@ -170,6 +170,8 @@ static Tuning read_tuning() {
 }
 
 struct vw_graph;
+struct vw_ctx;
+static void kill_pipelines_of(vw_ctx* c);
 
 struct vw_ctx {
   int device = 0;
@@ -466,6 +468,8 @@ extern "C" vw_status vw_ctx_destroy(vw_ctx* c) {
     c->capturing = false;
   }
   hipStreamSynchronize(c->stream);
+  kill_pipelines_of(c);
+  hipSetDevice(c->device);
   collect_timing(c);
   // graphs outliving their context: free their HIP objects now; the handles stay valid for
   // vw_graph_destroy, and vw_graph_launch on them fails with VW_ERR_STATE
@@ -623,6 +627,179 @@ extern "C" vw_status vw_graph_destroy(vw_graph* gr) {
   release_graph(gr);
   c->graphs.erase(gr);
   delete gr;
+  return ok();
+}
+
+// ------------------------------------------------------------------------------------------------
+// Pipelined round trips (include/vectorwave_amd.h "pipelined round trips").  Step i runs the forward
+// of buffer set i mod R on the forward context's stream and then, after an event, its inverse on the
+// inverse context's stream; step i's forward waits for step i - R's inverse (the set it overwrites).
+// So step i + 1's forward runs beside step i's inverse while every step still does its whole forward
+// and inverse.  The loop is issued here, in C++, so a small shard (the 8-GPU headline: 512 rows,
+// ~50 us of GPU work per step) is not limited by a Python caller's per-call overhead.
+struct vw_pipeline {
+  vw_ctx* cf = nullptr;
+  vw_ctx* ci = nullptr;
+  int device = 0;
+  int esz = 8;
+  int R = 0;
+  std::vector<void*> x, det, app, y;
+  int64_t B = 0, N = 0;
+  std::vector<double> lo, hi;
+  int L = 0, wavelet_id = 0, boundary = 0, J = 0;
+  unsigned flags = 0;
+  std::vector<hipEvent_t> ev_f, ev_i;
+  std::vector<char> live;
+  hipEvent_t join_ev = nullptr;
+  int64_t next = 0;       // index of the next step (selects its buffer set)
+  bool dead = false;      // a context was destroyed under it
+};
+
+static std::mutex g_pipe_mu;
+static std::set<vw_pipeline*> g_pipes;
+
+static void release_pipeline(vw_pipeline* p) {
+  for (auto e : p->ev_f) if (e) hipEventDestroy(e);
+  for (auto e : p->ev_i) if (e) hipEventDestroy(e);
+  if (p->join_ev) hipEventDestroy(p->join_ev);
+  p->ev_f.clear();
+  p->ev_i.clear();
+  p->join_ev = nullptr;
+}
+
+// vw_ctx_destroy: pipelines that use the context die with it (their events are freed, the handles
+// stay valid for vw_pipeline_destroy, vw_pipeline_run fails with VW_ERR_STATE)
+static void kill_pipelines_of(vw_ctx* c) {
+  std::lock_guard<std::mutex> g(g_pipe_mu);
+  for (vw_pipeline* p : g_pipes)
+    if (!p->dead && (p->cf == c || p->ci == c)) {
+      hipSetDevice(p->device);
+      hipStreamSynchronize(p->cf->stream);
+      hipStreamSynchronize(p->ci->stream);
+      release_pipeline(p);
+      p->dead = true;
+    }
+}
+
+extern "C" vw_status vw_pipeline_create(vw_ctx* cf, vw_ctx* ci, int elem_bytes, int sets, void* const* x,
+                                        void* const* details, void* const* approx, void* const* y, int64_t B,
+                                        int64_t N, const double* lo, const double* hi, int L, int wavelet_id,
+                                        int boundary, int J, unsigned flags, vw_pipeline** out) {
+  if (!cf || !ci || !x || !details || !approx || !y || !lo || !hi || !out) return fail(VW_ERR_NULL, "null argument");
+  if (elem_bytes != 8 && elem_bytes != 4) return fail(VW_ERR_ARG, "elem_bytes must be 8 (f64) or 4 (f32)");
+  if (sets < 1 || sets > 1024) return fail(VW_ERR_ARG, "sets must be in [1, 1024]");
+  if (B <= 0 || N <= 0) return fail(VW_ERR_EMPTY, "Signals cannot be null or empty");
+  if (L <= 0 || L > kMaxTaps) return fail(VW_ERR_ARG, "filter length %d out of range", L);
+  if (J < 1) return fail(VW_ERR_ARG, "levels must be >= 1");
+  if (cf->device != ci->device) return fail(VW_ERR_ARG, "both contexts must be on one device");
+  // calls that synchronize or stage host memory have no place in an asynchronous pipeline
+  if (flags & (VW_FLAG_HOST_MEMORY | VW_FLAG_SYNC | VW_FLAG_VALIDATE))
+    return fail(VW_ERR_ARG, "pipeline steps take device buffers, no SYNC / VALIDATE / HOST_MEMORY");
+  for (int r = 0; r < sets; ++r)
+    if (!x[r] || !details[r] || !approx[r] || !y[r]) return fail(VW_ERR_NULL, "buffer set %d has a null pointer", r);
+  if (cf->capturing || ci->capturing) return fail(VW_ERR_STATE, "a context is capturing");
+  vw_pipeline* p = new vw_pipeline();
+  p->cf = cf;
+  p->ci = ci;
+  p->device = cf->device;
+  p->esz = elem_bytes;
+  p->R = sets;
+  p->x.assign(x, x + sets);
+  p->det.assign(details, details + sets);
+  p->app.assign(approx, approx + sets);
+  p->y.assign(y, y + sets);
+  p->B = B;
+  p->N = N;
+  p->lo.assign(lo, lo + L);
+  p->hi.assign(hi, hi + L);
+  p->L = L;
+  p->wavelet_id = wavelet_id;
+  p->boundary = boundary;
+  p->J = J;
+  p->flags = flags;
+  hipSetDevice(p->device);
+  p->ev_f.assign(sets, nullptr);
+  p->ev_i.assign(sets, nullptr);
+  p->live.assign(sets, 0);
+  hipError_t e = hipEventCreateWithFlags(&p->join_ev, hipEventDisableTiming);
+  for (int r = 0; r < sets && e == hipSuccess; ++r) {
+    e = hipEventCreateWithFlags(&p->ev_f[r], hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&p->ev_i[r], hipEventDisableTiming);
+  }
+  if (e != hipSuccess) {
+    release_pipeline(p);
+    delete p;
+    return fail(VW_ERR_DEVICE, "event creation failed: %s", hipGetErrorString(e));
+  }
+  {
+    std::lock_guard<std::mutex> g(g_pipe_mu);
+    g_pipes.insert(p);
+  }
+  *out = p;
+  return ok();
+}
+
+extern "C" vw_status vw_pipeline_run(vw_pipeline* p, int64_t steps) {
+  if (!p) return fail(VW_ERR_NULL, "pipeline is null");
+  if (p->dead) return fail(VW_ERR_STATE, "a context of this pipeline was destroyed");
+  if (steps < 0) return fail(VW_ERR_ARG, "steps must be >= 0");
+  hipSetDevice(p->device);
+  const bool f32 = p->esz == 4;
+  for (int64_t k = 0; k < steps; ++k) {
+    const int r = (int)(p->next % p->R);
+    hipStream_t sf = p->cf->stream, si = p->ci->stream;
+    if (p->live[r]) VW_HIP(hipStreamWaitEvent(sf, p->ev_i[r], 0));
+    vw_status st = f32 ? vw_modwt_forward_f32(p->cf, (const float*)p->x[r], p->B, p->N, p->N, p->lo.data(),
+                                              p->hi.data(), p->L, p->wavelet_id, p->boundary, p->J, p->flags,
+                                              (float*)p->det[r], (float*)p->app[r])
+                       : vw_modwt_forward_f64(p->cf, (const double*)p->x[r], p->B, p->N, p->N, p->lo.data(),
+                                              p->hi.data(), p->L, p->wavelet_id, p->boundary, p->J, p->flags,
+                                              (double*)p->det[r], (double*)p->app[r]);
+    if (st != VW_OK) return st;
+    VW_HIP(hipEventRecord(p->ev_f[r], sf));
+    VW_HIP(hipStreamWaitEvent(si, p->ev_f[r], 0));
+    st = f32 ? vw_modwt_inverse_f32(p->ci, (const float*)p->det[r], (const float*)p->app[r], p->B, p->N,
+                                    p->lo.data(), p->hi.data(), p->L, p->wavelet_id, p->boundary, p->J, 0xFFFFFFFFu,
+                                    0, p->flags, (float*)p->y[r])
+             : vw_modwt_inverse_f64(p->ci, (const double*)p->det[r], (const double*)p->app[r], p->B, p->N,
+                                    p->lo.data(), p->hi.data(), p->L, p->wavelet_id, p->boundary, p->J, 0xFFFFFFFFu,
+                                    0, p->flags, (double*)p->y[r]);
+    if (st != VW_OK) return st;
+    VW_HIP(hipEventRecord(p->ev_i[r], si));
+    p->live[r] = 1;
+    ++p->next;
+  }
+  return ok();
+}
+
+extern "C" vw_status vw_pipeline_join(vw_pipeline* p) {
+  if (!p) return fail(VW_ERR_NULL, "pipeline is null");
+  if (p->dead) return fail(VW_ERR_STATE, "a context of this pipeline was destroyed");
+  hipSetDevice(p->device);
+  VW_HIP(hipEventRecord(p->join_ev, p->ci->stream));
+  VW_HIP(hipStreamWaitEvent(p->cf->stream, p->join_ev, 0));
+  std::fill(p->live.begin(), p->live.end(), 0);
+  return ok();
+}
+
+extern "C" int64_t vw_pipeline_last_set(vw_pipeline* p) {
+  if (!p || p->next == 0) return -1;
+  return (p->next - 1) % p->R;
+}
+
+extern "C" vw_status vw_pipeline_destroy(vw_pipeline* p) {
+  if (!p) return fail(VW_ERR_NULL, "pipeline is null");
+  {
+    std::lock_guard<std::mutex> g(g_pipe_mu);
+    g_pipes.erase(p);
+  }
+  if (!p->dead) {
+    hipSetDevice(p->device);
+    hipStreamSynchronize(p->cf->stream);
+    hipStreamSynchronize(p->ci->stream);
+    release_pipeline(p);
+  }
+  delete p;
   return ok();
 }
 
@@ -2183,7 +2360,11 @@ extern "C" vw_status vw_median_f64(vw_ctx* c, const double* x, int64_t B, int64_
       if (c->capturing)
         return fail(VW_ERR_STATE, "median scratch growth during capture: run the call once before capturing it");
       if (c->med) {
-        VW_HIP(hipStreamSynchronize(c->stream));  // only this context's stream ever uses the scratch
+        // the scratch may have been used on streams the context was bound to earlier, and graphs that
+        // recorded a centred median hold its address: drain the device and make those graphs stale
+        // (vw_graph_launch then refuses them with VW_ERR_STATE), as ensure_ws does for the workspace
+        hipDeviceSynchronize();
+        ++c->ws_gen;
         hipFree(c->med);
         c->med = nullptr;
         c->med_bytes = 0;

@@ -59,6 +59,16 @@ class Engine:
                 cls._instances[device] = eng
             return eng
 
+    def close(self) -> None:
+        """Destroy this context (vw_ctx_destroy: drains its stream, invalidates its graphs).  Not for the
+        shared instance of ``Engine.get``."""
+        if self.ctx:
+            with Engine._lock:
+                if Engine._instances.get(self.device) is self:
+                    del Engine._instances[self.device]
+            _check(self.lib.vw_ctx_destroy(self.ctx))
+            self.ctx = None
+
     # -- streams ------------------------------------------------------------------------------
     def bind_torch_stream(self) -> None:
         """Enqueue on torch's current stream of this device (orders engine work with torch ops)."""

@@ -129,7 +129,22 @@ class DeviceGroup:
         if len(parts) != len(self.engines):
             raise InvalidArgumentException("one (details, approx) pair per context")
         parts = [(d.contiguous(), a.contiguous()) for d, a in parts]
-        J, _, N = parts[0][0].shape
+        d0 = parts[0][0]
+        if d0.ndim != 3:
+            raise InvalidArgumentException("details must be [levels][rows][length]")
+        J, _, N = d0.shape
+        # every shard is checked before any launch: the engine reads these as float64
+        # [J][rows][N] / [rows][N] buffers on context k's device, so a mismatch would be an out-of-bounds
+        # access, not an error
+        for k, (d, a) in enumerate(parts):
+            dev = self.engines[k].device
+            ok = (d.dtype == torch.float64 and a.dtype == torch.float64 and d.ndim == 3 and a.ndim == 2
+                  and d.shape[0] == J and d.shape[2] == N and a.shape[1] == N and d.shape[1] == a.shape[0]
+                  and d.is_cuda and a.is_cuda and d.device.index == dev and a.device.index == dev)
+            if not ok:
+                raise InvalidArgumentException(
+                    f"parts[{k}] must be float64 details [{J}][rows][{N}] and approx [rows][{N}] on cuda:{dev}, got "
+                    f"{tuple(d.shape)} {d.dtype} {d.device} / {tuple(a.shape)} {a.dtype} {a.device}")
         ys = [torch.empty_like(a) for _, a in parts]
         rows = (ctypes.c_int64 * len(parts))(*[a.shape[0] for _, a in parts])
         lo, hi = wavelet.lowPassReconstruction(), wavelet.highPassReconstruction()
