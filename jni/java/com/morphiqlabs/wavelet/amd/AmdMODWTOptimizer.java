@@ -21,18 +21,8 @@ import com.morphiqlabs.wavelet.api.spi.MODWTOptimizer;
  * calls, so the provider is thread-safe.
  */
 public final class AmdMODWTOptimizer implements MODWTOptimizer {
-    private static final int DEVICE = Integer.getInteger("vectorwave.amd.device", 0);
-    private static final int FMA = Boolean.getBoolean("vectorwave.amd.fma") ? AmdNative.FLAG_FMA : 0;
-
-    private static final class Holder {  // lazily created, released at JVM exit
-        static final long CTX = AmdNative.LOADED ? AmdNative.ctxCreate(DEVICE) : 0L;
-
-        static {
-            if (CTX != 0L) {
-                Runtime.getRuntime().addShutdownHook(new Thread(() -> AmdNative.ctxDestroy(CTX)));
-            }
-        }
-    }
+    private static final int DEVICE = AmdRuntime.DEVICE;
+    private static final int FMA = AmdRuntime.FMA;
 
     /** Public no-argument constructor for ServiceLoader. */
     public AmdMODWTOptimizer() {}
@@ -40,7 +30,7 @@ public final class AmdMODWTOptimizer implements MODWTOptimizer {
     @Override
     public boolean isSupported() {
         try {
-            return AmdNative.LOADED && Holder.CTX != 0L;
+            return AmdRuntime.isAvailable();
         } catch (Throwable t) {
             return false;
         }
@@ -66,7 +56,7 @@ public final class AmdMODWTOptimizer implements MODWTOptimizer {
         final int n = signal.length;
         double[] approx = new double[n];
         double[] detail = new double[n];
-        AmdNative.check(AmdNative.modwt1Forward(Holder.CTX, signal, 1, n, wavelet.lowPassDecomposition(),
+        AmdNative.check(AmdNative.modwt1Forward(AmdRuntime.ctx(), signal, 1, n, wavelet.lowPassDecomposition(),
                 wavelet.highPassDecomposition(), AmdNative.boundary(boundaryMode),
                 AmdNative.FLAG_VALIDATE | FMA, approx, detail));
         return new Result(detail, approx);
@@ -83,7 +73,7 @@ public final class AmdMODWTOptimizer implements MODWTOptimizer {
         }
         final int n = scalingCoeffs.length;
         double[] y = new double[n];
-        AmdNative.check(AmdNative.modwt1Inverse(Holder.CTX, scalingCoeffs, waveletCoeffs, 1, n,
+        AmdNative.check(AmdNative.modwt1Inverse(AmdRuntime.ctx(), scalingCoeffs, waveletCoeffs, 1, n,
                 wavelet.lowPassReconstruction(), wavelet.highPassReconstruction(),
                 AmdNative.boundary(boundaryMode), FMA, y));
         return y;
@@ -106,25 +96,53 @@ public final class AmdMODWTOptimizer implements MODWTOptimizer {
         if (!equal) {
             return MODWTOptimizer.super.forwardBatch(signals, wavelet, boundaryMode);
         }
-        // flatten once (BatchMODWT.java:67-72 does the same), one device call for the whole batch
-        double[] flat = new double[B * n];
-        for (int b = 0; b < B; b++) {
-            System.arraycopy(signals[b], 0, flat, b * n, n);
-        }
-        double[] approx = new double[B * n];
-        double[] detail = new double[B * n];
-        AmdNative.check(AmdNative.modwt1Forward(Holder.CTX, flat, B, n, wavelet.lowPassDecomposition(),
-                wavelet.highPassDecomposition(), AmdNative.boundary(boundaryMode),
-                AmdNative.FLAG_VALIDATE | FMA, approx, detail));
+        // one device call per chunk of rows (BatchMODWT.java:67-72 flattens the same way); rows * n stays a
+        // valid Java array length -- B * n itself may exceed Integer.MAX_VALUE (ADVICE r4)
         MODWTOptimizedResult[] out = new MODWTOptimizedResult[B];
-        for (int b = 0; b < B; b++) {
-            double[] w = new double[n];
-            double[] v = new double[n];
-            System.arraycopy(detail, b * n, w, 0, n);
-            System.arraycopy(approx, b * n, v, 0, n);
-            out[b] = new Result(w, v);
+        final int rows = AmdBatchMODWT.chunkRows(n, B);
+        for (int b0 = 0; b0 < B; b0 += rows) {
+            final int nb = Math.min(rows, B - b0);
+            double[] flat = AmdBatchMODWT.flatten(signals, b0, nb, n);
+            double[] approx = new double[flat.length];
+            double[] detail = new double[flat.length];
+            AmdNative.check(AmdNative.modwt1Forward(AmdRuntime.ctx(), flat, nb, n, wavelet.lowPassDecomposition(),
+                    wavelet.highPassDecomposition(), AmdNative.boundary(boundaryMode),
+                    AmdNative.FLAG_VALIDATE | FMA, approx, detail));
+            for (int b = 0; b < nb; b++) {
+                double[] w = new double[n];
+                double[] v = new double[n];
+                System.arraycopy(detail, b * n, w, 0, n);
+                System.arraycopy(approx, b * n, v, 0, n);
+                out[b0 + b] = new Result(w, v);
+            }
         }
         return out;
+    }
+
+    /**
+     * Multi-level batch forward, BatchMODWT.multiLevelAoS semantics (ext/extensions/modwt/BatchMODWT.java:90-111:
+     * PERIODIC, no level cap).  Not part of the reference's SPI: jni/reference/activate-amd-optimizer.patch adds
+     * it to MODWTOptimizer as a default method returning null ("not handled") and makes BatchMODWT.multiLevelAoS
+     * ask the registered optimizer first; with that patch applied this method overrides the default.
+     * Returns the details [levels][batch][length] and fills finalApproxOut [batch][length].
+     */
+    public double[][][] forwardMultiLevelBatch(double[][] signals, Wavelet wavelet, int levels,
+                                               double[][] finalApproxOut) {
+        if (!(wavelet instanceof com.morphiqlabs.wavelet.api.DiscreteWavelet dw)) {
+            return null;   // not handled: the reference path runs
+        }
+        var r = AmdBatchMODWT.multiLevelAoS(dw, signals, levels);
+        double[][] approx = r.finalApprox();
+        for (int b = 0; b < finalApproxOut.length; b++) finalApproxOut[b] = approx[b];
+        return r.detailPerLevel();
+    }
+
+    /** Multi-level batch inverse, BatchMODWT.inverseMultiLevelAoS semantics (:151-178); see above. */
+    public double[][] inverseMultiLevelBatch(double[][][] detailPerLevel, double[][] finalApprox, Wavelet wavelet) {
+        if (!(wavelet instanceof com.morphiqlabs.wavelet.api.DiscreteWavelet dw)) {
+            return null;
+        }
+        return AmdBatchMODWT.inverseMultiLevelAoS(dw, detailPerLevel, finalApprox);
     }
 
     private record Result(double[] wavelet, double[] scaling) implements MODWTOptimizedResult {

@@ -84,6 +84,15 @@ public final class AmdNative {
                                      int boundary, int levels, int method, double fixedThreshold, boolean soft,
                                      int flags, double[] y, double[] thresholdsOut);
 
+    // AoS batches as the Java API holds them (double[][] signals, double[][][] details [levels][batch][length]):
+    // rows gathered / scattered by the native side in chunks (no flattening here, no int-sized B*N product)
+    static native int modwtForwardAoS(long ctx, double[][] x, double[] lo, double[] hi, int waveletId, int boundary,
+                                      int J, int flags, double[][][] details, double[][] approx);
+    static native int modwtInverseAoS(long ctx, double[][][] details, double[][] approx, double[] lo, double[] hi,
+                                      int waveletId, int boundary, int flags, double[][] y);
+    static native int swtDenoiseAoS(long ctx, double[][] x, double[] lo, double[] hi, int waveletId, int boundary,
+                                    int J, double threshold, boolean soft, int flags, double[][] y);
+
     // direct (off-heap) buffers, native byte order: no copy, no pinning
     static native int modwtForwardDirect(long ctx, ByteBuffer x, int B, int N, double[] lo, double[] hi,
                                          int waveletId, int boundary, int J, int flags, ByteBuffer details,

@@ -294,3 +294,154 @@ JNIEXPORT jint JNICALL VW_JNI(modwtInverseDirect)(JNIEnv *e, jclass c, jlong ctx
   return vw_modwt_inverse_f64(CTX(ctx), pd, pa, B, N, tl.v, th.v, tl.n, wid, boundary, J, 0xFFFFFFFFu, 0,
                               (unsigned)flags | HOST_FLAGS, py);
 }
+
+/* ---- AoS batches: double[][] rows straight into the engine's staging ------------------------
+ * BatchMODWT.multiLevelAoS / inverseMultiLevelAoS (ext/extensions/modwt/BatchMODWT.java:90-111,
+ * :151-178) and VectorWaveSwtAdapter.denoise over a batch.  The Java side passes its double[][] (and
+ * double[][][] for the details) unchanged: rows are gathered into one native block per chunk
+ * (GetDoubleArrayRegion per row -- the only copy; no Java-side flattening, no array pinned across the
+ * GPU call) and the results scattered back row by row.  Chunks of rows keep each native block under
+ * kChunkBytes and every size in size_t, so a batch whose B*N or J*B*N exceeds Integer.MAX_VALUE (a
+ * Java array's limit, e.g. 256 x 2^20 x 10 details) still goes through.  Row lengths are checked here
+ * too (VW_ERR_ARG), the Java facade validates first with the reference's messages.  Local references
+ * are released per row: the JNI guarantees only 16. */
+static const size_t kChunkBytes = (size_t)512 << 20;
+
+static jsize chunk_rows(size_t per_row_doubles, jsize B) {
+  size_t r = kChunkBytes / (per_row_doubles * sizeof(double));
+  if (r < 1) r = 1;
+  return r < (size_t)B ? (jsize)r : B;
+}
+
+/* rows[b0 .. b0+nb) (each of length n) <-> dst[nb][n]; 0 on a null row or a length mismatch */
+static int gather_rows(JNIEnv *e, jobjectArray rows, jsize b0, jsize nb, jsize n, double *dst) {
+  for (jsize b = 0; b < nb; ++b) {
+    jdoubleArray r = (jdoubleArray)(*e)->GetObjectArrayElement(e, rows, b0 + b);
+    if (!r) return 0;
+    int ok = (*e)->GetArrayLength(e, r) == n;
+    if (ok) (*e)->GetDoubleArrayRegion(e, r, 0, n, dst + (size_t)b * (size_t)n);
+    (*e)->DeleteLocalRef(e, r);
+    if (!ok) return 0;
+  }
+  return 1;
+}
+
+static int scatter_rows(JNIEnv *e, jobjectArray rows, jsize b0, jsize nb, jsize n, const double *src) {
+  for (jsize b = 0; b < nb; ++b) {
+    jdoubleArray r = (jdoubleArray)(*e)->GetObjectArrayElement(e, rows, b0 + b);
+    if (!r) return 0;
+    int ok = (*e)->GetArrayLength(e, r) == n;
+    if (ok) (*e)->SetDoubleArrayRegion(e, r, 0, n, src + (size_t)b * (size_t)n);
+    (*e)->DeleteLocalRef(e, r);
+    if (!ok) return 0;
+  }
+  return 1;
+}
+
+/* level plane l of a double[][][] ([levels][batch][length]) */
+static jobjectArray plane(JNIEnv *e, jobjectArray dpl, jsize l) {
+  return (jobjectArray)(*e)->GetObjectArrayElement(e, dpl, l);
+}
+
+static jsize row_len(JNIEnv *e, jobjectArray rows) {
+  if (!rows || (*e)->GetArrayLength(e, rows) < 1) return -1;
+  jdoubleArray r = (jdoubleArray)(*e)->GetObjectArrayElement(e, rows, 0);
+  if (!r) return -1;
+  jsize n = (*e)->GetArrayLength(e, r);
+  (*e)->DeleteLocalRef(e, r);
+  return n;
+}
+
+JNIEXPORT jint JNICALL VW_JNI(modwtForwardAoS)(JNIEnv *e, jclass c, jlong ctx, jobjectArray x, jdoubleArray lo,
+                                               jdoubleArray hi, jint wid, jint boundary, jint J, jint flags,
+                                               jobjectArray details, jobjectArray approx) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n || J < 1) return VW_ERR_ARG;
+  if (!x || !details || !approx) return VW_ERR_NULL;
+  const jsize B = (*e)->GetArrayLength(e, x), N = row_len(e, x);
+  if (N < 1) return VW_ERR_EMPTY;
+  if ((*e)->GetArrayLength(e, details) != J || (*e)->GetArrayLength(e, approx) != B) return VW_ERR_ARG;
+  const jsize CB = chunk_rows((size_t)(J + 2) * (size_t)N, B);
+  int oom = 0;
+  double *px = out_buf(0, (size_t)CB * N, &oom), *pd = out_buf(1, (size_t)J * CB * N, &oom);
+  double *pa = out_buf(2, (size_t)CB * N, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = VW_OK;
+  for (jsize b0 = 0; b0 < B && st == VW_OK; b0 += CB) {
+    const jsize nb = B - b0 < CB ? B - b0 : CB;
+    if (!gather_rows(e, x, b0, nb, N, px)) { st = VW_ERR_ARG; break; }
+    st = vw_modwt_forward_f64(CTX(ctx), px, nb, N, N, tl.v, th.v, tl.n, wid, boundary, J,
+                              (unsigned)flags | HOST_FLAGS, pd, pa);
+    if (st != VW_OK) break;
+    for (jsize l = 0; l < J && st == VW_OK; ++l) {
+      jobjectArray pl = plane(e, details, l);
+      if (!pl || !scatter_rows(e, pl, b0, nb, N, pd + (size_t)l * nb * N)) st = VW_ERR_ARG;
+      if (pl) (*e)->DeleteLocalRef(e, pl);
+    }
+    if (st == VW_OK && !scatter_rows(e, approx, b0, nb, N, pa)) st = VW_ERR_ARG;
+  }
+  trim_slots();
+  return st;
+}
+
+JNIEXPORT jint JNICALL VW_JNI(modwtInverseAoS)(JNIEnv *e, jclass c, jlong ctx, jobjectArray details,
+                                               jobjectArray approx, jdoubleArray lo, jdoubleArray hi, jint wid,
+                                               jint boundary, jint flags, jobjectArray y) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n) return VW_ERR_ARG;
+  if (!details || !approx || !y) return VW_ERR_NULL;
+  const jsize J = (*e)->GetArrayLength(e, details), B = (*e)->GetArrayLength(e, approx), N = row_len(e, approx);
+  if (J < 1) return VW_ERR_ARG;
+  if (N < 1) return VW_ERR_EMPTY;
+  if ((*e)->GetArrayLength(e, y) != B) return VW_ERR_ARG;
+  const jsize CB = chunk_rows((size_t)(J + 2) * (size_t)N, B);
+  int oom = 0;
+  double *pd = out_buf(0, (size_t)J * CB * N, &oom), *pa = out_buf(1, (size_t)CB * N, &oom);
+  double *py = out_buf(2, (size_t)CB * N, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = VW_OK;
+  for (jsize b0 = 0; b0 < B && st == VW_OK; b0 += CB) {
+    const jsize nb = B - b0 < CB ? B - b0 : CB;
+    for (jsize l = 0; l < J && st == VW_OK; ++l) {
+      jobjectArray pl = plane(e, details, l);
+      if (!pl || (*e)->GetArrayLength(e, pl) != B || !gather_rows(e, pl, b0, nb, N, pd + (size_t)l * nb * N))
+        st = VW_ERR_ARG;
+      if (pl) (*e)->DeleteLocalRef(e, pl);
+    }
+    if (st != VW_OK) break;
+    if (!gather_rows(e, approx, b0, nb, N, pa)) { st = VW_ERR_ARG; break; }
+    st = vw_modwt_inverse_f64(CTX(ctx), pd, pa, nb, N, tl.v, th.v, tl.n, wid, boundary, J, 0xFFFFFFFFu, 0,
+                              (unsigned)flags | HOST_FLAGS, py);
+    if (st == VW_OK && !scatter_rows(e, y, b0, nb, N, py)) st = VW_ERR_ARG;
+  }
+  trim_slots();
+  return st;
+}
+
+JNIEXPORT jint JNICALL VW_JNI(swtDenoiseAoS)(JNIEnv *e, jclass c, jlong ctx, jobjectArray x, jdoubleArray lo,
+                                             jdoubleArray hi, jint wid, jint boundary, jint J, jdouble threshold,
+                                             jboolean soft, jint flags, jobjectArray y) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n) return VW_ERR_ARG;
+  if (!x || !y) return VW_ERR_NULL;
+  const jsize B = (*e)->GetArrayLength(e, x), N = row_len(e, x);
+  if (N < 1) return VW_ERR_EMPTY;
+  if ((*e)->GetArrayLength(e, y) != B) return VW_ERR_ARG;
+  const jsize CB = chunk_rows(2 * (size_t)N, B);
+  int oom = 0;
+  double *px = out_buf(0, (size_t)CB * N, &oom), *py = out_buf(1, (size_t)CB * N, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = VW_OK;
+  for (jsize b0 = 0; b0 < B && st == VW_OK; b0 += CB) {
+    const jsize nb = B - b0 < CB ? B - b0 : CB;
+    if (!gather_rows(e, x, b0, nb, N, px)) { st = VW_ERR_ARG; break; }
+    st = vw_swt_denoise_f64(CTX(ctx), px, nb, N, N, tl.v, th.v, tl.n, wid, boundary, J, threshold, soft ? 1 : 0,
+                            (unsigned)flags | HOST_FLAGS, py, NULL);
+    if (st == VW_OK && !scatter_rows(e, y, b0, nb, N, py)) st = VW_ERR_ARG;
+  }
+  trim_slots();
+  return st;
+}
