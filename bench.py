@@ -658,7 +658,9 @@ def plan_schedule(args, rows, N, esz, cus, pipeline):
 
     Contexts per GPU: K parts of the rows, each on its own context + stream (--contexts; 0 = policy: 2
     above 2 signals per CU -- measured on MI355X, db4 4096 x 4096: 43.6-44.0K -> 44.7-45.7K; 1024 rows:
-    39.4K -> 44.1K; 512 rows: 37.0K -> 36.1K, profiles/r03/ab_contexts.log).
+    39.4K -> 44.1K; 512 rows: 37.0K -> 36.1K, profiles/r03/ab_contexts.log; 4 at >= 16 signals per CU of
+    <= 4096 samples -- round 5, same box, three alternations, db4 4096 x 4096: 2 contexts 45.2-45.6K, 3
+    45.1-46.5K, 4 46.0-46.5K, 8 45.3-45.5K, profiles/r05/ab_contexts_4096.log).
 
     Buffer sets: with one set the same 128 MiB input was re-read every step and stayed in
     the Infinity Cache (the persistent forward's LDS-DMA allocates there, the streaming loads and stores
@@ -676,7 +678,7 @@ def plan_schedule(args, rows, N, esz, cus, pipeline):
     signals the one-workgroup-per-signal kernels hold (N <= 16384): the long-signal kernels tile every
     signal over many workgroups, and db8-stream (256 x 2^20) runs 15.1-15.3K sequentially vs 14.7-14.8K
     overlapped (profiles/r04/ab_schedule_db8.log)."""
-    K = args.contexts or (2 if rows > 2 * cus else 1)
+    K = args.contexts or (4 if rows >= 16 * cus and N <= 4096 else 2 if rows > 2 * cus else 1)
     R = args.rotate or max(2, -(-(512 << 20) // max(rows * N * esz, 1)))
     rot = (R, bool(args.rotate_outputs or not args.rotate))
     overlap = pipeline == "fwd+inv" and (args.overlap_steps or (not args.contexts and rows <= 2 * cus and N <= 16384))

@@ -4,7 +4,7 @@
 set -e
 ROOT="$(cd "$(dirname "$0")/.." && pwd)"
 NAME=$1; EXTRA=$2; TAPS=${3:-X(8)}
-D="$ROOT/build/var_$NAME"
+D="$ROOT/${VARDIR:-build}/var_$NAME"
 mkdir -p "$D/src/csrc" "$D/include"
 cp "$ROOT"/vectorwave_amd/csrc/* "$D/src/csrc/" 2>/dev/null || true
 rm -f "$D"/src/csrc/*.o

@@ -1,7 +1,7 @@
+# round-5: compile-time tap offsets in the deep forward (VW_DEEP_CK) and the inverse multi-level tiles (VW_MULTI_CK)
+# -- parity on the product build, then same-box A/B: ck0 (both runtime), mck0 (deep only), ck1 (both)
 set -u
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
-mkdir -p gpurun_out/r5b
-bash tools/gpu_steps.sh t:test_gpu_pipeline.py t:test_gpu_graph.py t:test_gpu_multidevice.py || exit $?
-export AB_p512_V="|--batch 512;|--batch 512 --contexts 1" AB_p512_STEPS=200 AB_p512_REPS=3
-export AB_p4k_V="|" AB_p4k_STEPS=20 AB_p4k_REPS=2
-bash tools/gpu_steps.sh ab:p512 ab:p4k "bench:--batch 512 --steps 200 --no-cpu-baseline --no-alt"
+bash tools/gpu_steps.sh t:test_gpu_deep.py t:config4 t:multilevel || exit $?
+export AB_ck_V="VW_LIB_PATH=vwvar/var_ck0/libvectorwave_amd.so|;VW_LIB_PATH=vwvar/var_mck0/libvectorwave_amd.so|;VW_LIB_PATH=vwvar/var_ck1/libvectorwave_amd.so|" AB_ck_STEPS=10 AB_ck_REPS=3 AB_ck_CFG=db8-stream
+bash tools/gpu_steps.sh ab:ck

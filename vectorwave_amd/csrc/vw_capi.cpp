@@ -1578,10 +1578,12 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
           const int nvmax = (mtile + m.ext[g - 1]) / V + 1;
           m.region = (nvmax + nvmax / 8 + 1) * V;
         }
+        // slack past D for the compile-time-stride reads (vw_device.h k_inverse_multi): 15*M <= 120 vectors
+        m.slack = 160;
         copy_taps(m.lo, lo, L);
         copy_taps(m.hi, hi, L);
         LaunchTimer lt(c, "inverse_level");
-        hipError_t e = launch_inverse_multi<T>(m, (int)(2 * m.region * sizeof(T)), fma, c->stream);
+        hipError_t e = launch_inverse_multi<T>(m, (int)((2 * m.region + m.slack * V) * sizeof(T)), fma, c->stream);
         if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse multi-level launch failed: %s", hipGetErrorString(e));
         cur = m.out_a;
         j = j0;

@@ -44,6 +44,15 @@ __device__ __forceinline__ void deep_store(T* dst, const vec& v) {
   else if constexpr (VW_DEEP_STORE == 2) *reinterpret_cast<vec*>(dst) = v;
 }
 constexpr int kDeepThreads = 256;
+// Forward levels 0..4 of a deep group with compile-time spacing (immediate LDS offsets); 0: runtime form only
+#ifndef VW_DEEP_CK
+#define VW_DEEP_CK 1
+#endif
+#ifndef VW_DEEP_TC
+#define VW_DEEP_TC 8   // taps whose LDS reads the no-wrap forward loop issues before their FMAs
+#endif
+constexpr int kDeepTC = VW_DEEP_TC;
+
 
 // One wave's LDS-DMA of 16 positions x 64 bytes (1 KiB): lane -> position lane / 4, 16-byte chunk lane % 4.
 template <typename T>
@@ -180,19 +189,82 @@ __global__ void __launch_bounds__(kDeepThreads) k_forward_deep(const DeepArgs<T>
       for (int r = 0; r < NP; ++r)
 #pragma unroll
         for (int e = 0; e < V; ++e) { al[r][e] = T(0); ah[r][e] = T(0); }
+      // tap i reads slot br - i*sk (mod cap), i ascending; the products are the same in every form below
+      auto fma2 = [&](int r, int i, const vec& x) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < L; ++i) {
+        for (int e = 0; e < V; ++e) {
+          al[r][e] = madd<FMA>(al[r][e], x[e], p.lo[i]);
+          ah[r][e] = madd<FMA>(ah[r][e], x[e], p.hi[i]);
+        }
+      };
+      // Compile-time spacing (the first kDeepCK levels of a group): the reads of a lane sit at fixed
+      // distances (L-1-i)*SK positions above a0 = slot br - (L-1)*SK, so each is ONE ds_read at an
+      // immediate offset from a0 -- or from a1 = a0 + cap where that slot wrapped (br < i*SK: one compare
+      // and select per read).  A wave whose lanes never wrap at this level takes the select-free loop.
+      // The runtime form (wrap arithmetic per read: sub, compare, select, address) measured ~1 INT32 VALU
+      // per FMA on db8-stream's levels 6..10 (profiles/r05/pmc_mix_db8_a0b973e.txt).
+      auto taps_c = [&](auto kc) __attribute__((always_inline)) {
+        constexpr int SK = 1 << decltype(kc)::value;
+        const T* a0[NP];
+        const T* a1[NP];
+        bool nowrap = true;
 #pragma unroll
         for (int r = 0; r < NP; ++r) {
-          int sl = br[r] - i * sk;
-          sl = sl < 0 ? sl + cap : sl;
-          const vec x = *reinterpret_cast<const vec*>(ring + sl * C);
-#pragma unroll
-          for (int e = 0; e < V; ++e) {
-            al[r][e] = madd<FMA>(al[r][e], x[e], p.lo[i]);
-            ah[r][e] = madd<FMA>(ah[r][e], x[e], p.hi[i]);
-          }
+          a0[r] = ring + (br[r] - (L - 1) * SK) * C;
+          a1[r] = a0[r] + cap * C;
+          nowrap = nowrap && br[r] >= (L - 1) * SK;
         }
+        if (__all(nowrap)) {
+          // 32-bit LDS base per lane, laundered so the compiler keeps it (and the positive immediate
+          // offsets) instead of re-basing on the highest tap with negative adds; the reads of a chunk of
+          // kDeepTC taps are issued together (VGPRs to spare at two workgroups per CU), then its FMAs
+          unsigned ab[NP];
+#pragma unroll
+          for (int r = 0; r < NP; ++r) {
+            ab[r] = (unsigned)(uintptr_t)a0[r];
+            asm volatile("" : "+v"(ab[r]));
+          }
+          static_for<0, (L + kDeepTC - 1) / kDeepTC>([&](auto c) __attribute__((always_inline)) {
+            constexpr int I0 = decltype(c)::value * kDeepTC;
+            constexpr int I1 = (I0 + kDeepTC < L) ? I0 + kDeepTC : L;
+            vec xs[I1 - I0][NP];
+#pragma unroll
+            for (int i = I0; i < I1; ++i)
+#pragma unroll
+              for (int r = 0; r < NP; ++r)
+                xs[i - I0][r] = lds_vec_at<vec>(ab[r] + (unsigned)((L - 1 - i) * SK * C * (int)sizeof(T)));
+#pragma unroll
+            for (int i = I0; i < I1; ++i)
+#pragma unroll
+              for (int r = 0; r < NP; ++r) fma2(r, i, xs[i - I0][r]);
+          });
+        } else {
+#pragma unroll
+          for (int i = 0; i < L; ++i)
+#pragma unroll
+            for (int r = 0; r < NP; ++r) {
+              const T* a = br[r] >= i * SK ? a0[r] : a1[r];
+              fma2(r, i, *reinterpret_cast<const vec*>(a + (L - 1 - i) * SK * C));
+            }
+        }
+      };
+      switch (VW_DEEP_CK ? k : -1) {
+        case 0: taps_c(std::integral_constant<int, 0>{}); break;
+        case 1: taps_c(std::integral_constant<int, 1>{}); break;
+        case 2: taps_c(std::integral_constant<int, 2>{}); break;
+        case 3: taps_c(std::integral_constant<int, 3>{}); break;
+        case 4: taps_c(std::integral_constant<int, 4>{}); break;
+        default:
+#pragma unroll
+          for (int i = 0; i < L; ++i) {
+#pragma unroll
+            for (int r = 0; r < NP; ++r) {
+              int sl = br[r] - i * sk;
+              sl = sl < 0 ? sl + cap : sl;
+              fma2(r, i, *reinterpret_cast<const vec*>(ring + sl * C));
+            }
+          }
+          break;
       }
 #pragma unroll
       for (int r = 0; r < NP; ++r)

@@ -106,6 +106,23 @@ __device__ __forceinline__ int sym_index(int idx, int n) {
 // lets global stores and prefetch loads stay in flight across it.  (__syncthreads() also waits
 // vmcnt(0), which would expose the latency of every detail-level store at every level.)  Values
 // loaded from global memory are waited for by the compiler at their first use, as usual.
+// 16-byte LDS read at a 32-bit LDS byte address.  With the base laundered (lds_base) the compiler keeps
+// base + constant as ONE ds_read with the constant in its offset field, instead of re-basing on the
+// highest address of a run of reads and paying a v_add per read.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Wint-to-pointer-cast"
+template <typename vec>
+__device__ __forceinline__ vec lds_vec_at(unsigned a) {
+  return *(const __attribute__((address_space(3))) vec*)a;
+}
+#pragma clang diagnostic pop
+template <typename T>
+__device__ __forceinline__ unsigned lds_base(const T* p) {
+  unsigned a = (unsigned)(uintptr_t)p;
+  asm volatile("" : "+v"(a));
+  return a;
+}
+
 __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt untouched
@@ -2301,6 +2318,9 @@ __global__ void __launch_bounds__(256) k_forward_multi(const MultiArgs<T> p) {
 // Inverse: A = a_j, D = d_j (thresholded on load for denoise); a_{j-1} is computed into registers
 // (kMultiInvNI vectors per thread) and written over A after a barrier -- two LDS regions, so four
 // 256-thread workgroups fit a CU (a third region for a_{j-1} measured 1.2x slower: two per CU).
+#ifndef VW_MULTI_CK
+#define VW_MULTI_CK 1  // k_inverse_multi register-blocked levels: compile-time strides, immediate LDS offsets
+#endif
 template <typename T, int L, bool FMA>
 __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
   constexpr int V = VT<T>::V;
@@ -2421,21 +2441,69 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
 #pragma unroll
           for (int e = 0; e < V; ++e) acc[r][e] = T(0);
         if (pr < pairs) {
+          // compile-time stride M (padded iff PD): the reads of a lane sit at fixed offsets off(j) from
+          // phys(vb) -- (vb & 7) + (M*j & 7) < 8 for every M <= 8 here (vb % 8 = pr % M < M, NI = 8), so
+          // (vb + M*j) >> 3 = (vb >> 3) + (M*j >> 3) -- and each is one ds_read at an immediate offset.
+          // Reads past the region end (at most 15*M vectors, only for outputs that are never stored) stay
+          // inside the allocation: the host adds p.slack >= 16*8 + 16 vectors after D (M <= 8 here).
+          const T* const tlo = p.lo;
+          const T* const thi = p.hi;
+          auto blk_c = [&](auto mc, auto pdc) __attribute__((always_inline)) {
+            constexpr int M = decltype(mc)::value;
+            constexpr bool PD = decltype(pdc)::value;
+            constexpr auto off = [](int j) { return PD ? M * j + ((M * j) >> 3) : M * j; };
 #pragma unroll
-          for (int br = 0; br < 2; ++br) {
-            const T* buf = br == 0 ? A : D;
-            const T* f = br == 0 ? p.lo : p.hi;
+            for (int br = 0; br < 2; ++br) {
+              const unsigned ab = lds_base((br == 0 ? A : D) + phys(vb, PD) * V);
 #pragma unroll
-            for (int j = 0; j < NI + L - 1; ++j) {
-              const vec x = *reinterpret_cast<const vec*>(buf + phys(min(vb + m * j, lim), pdk) * V);
+              for (int j = 0; j < NI + L - 1; ++j) {
+                const vec x = lds_vec_at<vec>(ab + (unsigned)(off(j) * V * (int)sizeof(T)));
 #pragma unroll
-              for (int r = 0; r < NI; ++r) {
-                const int i = j - r;
-                if (i >= 0 && i < L)
+                for (int r = 0; r < NI; ++r) {
+                  const int i = j - r;
+                  if (i >= 0 && i < L) {
+                    // the tap straight from the kernel arguments (a pointer to p.lo / p.hi would copy
+                    // the argument block to scratch)
+                    const T fi = br == 0 ? tlo[i] : thi[i];
 #pragma unroll
-                  for (int e = 0; e < V; ++e) acc[r][e] = madd<FMA>(acc[r][e], x[e], f[i]);
+                    for (int e = 0; e < V; ++e) acc[r][e] = madd<FMA>(acc[r][e], x[e], fi);
+                  }
+                }
+                if ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bounded reads in flight (VGPRs)
               }
             }
+          };
+          using I1 = std::integral_constant<int, 1>;
+          using I2 = std::integral_constant<int, 2>;
+          using I4 = std::integral_constant<int, 4>;
+          using I8 = std::integral_constant<int, 8>;
+          using BT = std::true_type;
+          // padded layouts only (the default, p.pad): more instantiations in this function raised it from 160
+          // VGPRs to 238 + 1.3 KiB of scratch (the taps, hoisted across the switch)
+          const int sel = VW_MULTI_CK && p.slack && pdk ? m : -1;
+          switch (sel) {
+            case 1: blk_c(I1{}, BT{}); break;
+            case 2: blk_c(I2{}, BT{}); break;
+            case 4: blk_c(I4{}, BT{}); break;
+            case 8: blk_c(I8{}, BT{}); break;
+            default:
+#pragma unroll
+              for (int br = 0; br < 2; ++br) {
+                const T* buf = br == 0 ? A : D;
+                const T* f = br == 0 ? p.lo : p.hi;
+#pragma unroll
+                for (int j = 0; j < NI + L - 1; ++j) {
+                  const vec x = *reinterpret_cast<const vec*>(buf + phys(min(vb + m * j, lim), pdk) * V);
+#pragma unroll
+                  for (int r = 0; r < NI; ++r) {
+                    const int i = j - r;
+                    if (i >= 0 && i < L)
+#pragma unroll
+                      for (int e = 0; e < V; ++e) acc[r][e] = madd<FMA>(acc[r][e], x[e], f[i]);
+                  }
+                }
+              }
+              break;
           }
           if (k == 0) {
 #pragma unroll

@@ -160,6 +160,7 @@ struct MultiArgs {
   int rblk;                  // inverse: register-blocked taps where S is a multiple of V
   int pf;                    // inverse: next level's detail tile prefetched into registers
   int pad;                   // inverse: padded LDS layout at the register-blocked levels (needs pf, rblk)
+  int slack;                 // inverse: LDS vectors allocated past D (compile-time-stride reads, 0 = off)
   T lo[kMaxTaps];
   T hi[kMaxTaps];
 };
