@@ -113,6 +113,8 @@ def parse(argv=None):
                         "left in the 256 MiB Infinity Cache; 0 = auto (R * input bytes >= 512 MiB, R >= 2, "
                         "outputs rotated too); 1 = one set (the round-1..3 method)")
     p.add_argument("--rotate-outputs", action="store_true", help="explicit --rotate R: rotate the outputs too")
+    p.add_argument("--no-isolated", action="store_true",
+                   help="skip the isolated per-pass kernel timing reported in roofline.isolated")
     p.add_argument("--overlap-steps", action="store_true",
                    help="pipeline step i+1's forward with step i's inverse on two contexts (rotated buffer sets); "
                         "default when the rank has <= 2 signals per CU and --contexts is not given")
@@ -366,9 +368,10 @@ class Part:
         if st != 0:
             raise RuntimeError(f"engine status {st}: {self.nat.last_error()}")
 
-    def step_fn(self, flags):
+    def step_fn(self, flags, only=None):
         """One step of this part: the config's passes over its rows, as C-ABI calls on its context.
-        Returns step(i): step i works on buffer set i mod R."""
+        Returns step(i): step i works on buffer set i mod R.  only="forward" / "inverse" (fwd+inv, for the
+        isolated kernel timing): that pass alone (the inverse reads the coefficients a full step left)."""
         nat, lib, w, J, N, B = self.nat, self.lib, self.w, self.J, self.N, self.rows
         p = lambda t: c_void_p(t.data_ptr())  # noqa: E731
         ctx = self.eng.ctx
@@ -381,10 +384,12 @@ class Part:
                 r = i % self.rotate
                 self.last = r
                 xp, dp, ap, yp = ptrs[r]
-                self._check(fwd(ctx, xp, B, N, N, self.lo_a, self.hi_a, self.L, w.wavelet_id, nat.PERIODIC, J, flags,
-                                dp, ap))
-                self._check(inv(ctx, dp, ap, B, N, self.lo_a, self.hi_a, self.L, w.wavelet_id, nat.PERIODIC, J,
-                                0xFFFFFFFF, 0, flags, yp))
+                if only != "inverse":
+                    self._check(fwd(ctx, xp, B, N, N, self.lo_a, self.hi_a, self.L, w.wavelet_id, nat.PERIODIC, J,
+                                    flags, dp, ap))
+                if only != "forward":
+                    self._check(inv(ctx, dp, ap, B, N, self.lo_a, self.hi_a, self.L, w.wavelet_id, nat.PERIODIC, J,
+                                    0xFFFFFFFF, 0, flags, yp))
             return step
         ptrs = [(p(s["x"]), p(s["y"]), p(s["thr"])) for s in self.sets]
 
@@ -484,7 +489,7 @@ PASS_FAMILIES = {"forward": ("forward", "forward_level"), "inverse": ("inverse",
 FAMILIES = ("forward", "inverse", "sigma", "forward_level", "inverse_level")
 
 
-def measure(torch, dist, world, wl, flags, mode, steps, warmup, settle_s, events):
+def measure(torch, dist, world, wl, flags, mode, steps, warmup, settle_s, events, only=None):
     """Settle, warm up, then time exactly `steps` steps between barrier + synchronize.
 
     Every part records its steps into HIP graphs on its own context and stream; the main stream forks
@@ -503,7 +508,7 @@ def measure(torch, dist, world, wl, flags, mode, steps, warmup, settle_s, events
         return (el, host_el), (settle_s, 0), {}, 0, {}
     parts = wl.parts
     main = torch.cuda.current_stream()
-    fns = [pt.step_fn(flags) for pt in parts]
+    fns = [pt.step_fn(flags, only) for pt in parts]
 
     def fork_join(fn):
         # the part on the main stream itself needs no fork / join (no cross-stream latency at K = 1)
@@ -770,6 +775,26 @@ def run(args, world, rank, local):
                                                   args.warmup, min(args.settle, 0.5), events)
         wk1.close()
         del wk1
+    # Isolated pass timing (fwd+inv): each pass alone, its launches back to back over the rotated buffer sets,
+    # so a launch's duration holds its own traffic only -- in the step, the inverse also absorbs the write-back
+    # of the forward's coefficient rows (sc1 stores) that drains while it runs.  Reported beside the roofline,
+    # not in place of it.
+    iso = None
+    if events and pipeline == "fwd+inv" and not args.no_isolated:
+        wki = Workload(engines[:1], streams[:1], w, J, rows, N, dtype, pipeline, start, torch, *rot)
+        prime = wki.parts[0].step_fn(flags)
+        with torch.cuda.stream(wki.parts[0].stream):
+            for r in range(wki.parts[0].rotate):
+                prime(r)   # every set holds the coefficients of its input
+        torch.cuda.synchronize()
+        iso = {}
+        for fam in ("forward", "inverse"):
+            _, _, _, _, ipass = measure(torch, dist, world, wki, flags, args.launch, args.steps, args.warmup,
+                                        min(args.settle, 0.3), events, only=fam)
+            if fam in ipass:
+                iso[fam] = ipass[fam]
+        wki.close()
+        del wki
     kkernels = {k: {"launches_per_step": round(n / max(ksampled, 1), 3), "ms_per_launch": round(ms / n, 5)}
                 for k, (ms, n) in kfams.items()}
     # algorithmic flops per pass: every level applies both filters, L taps each, one FMA (2 flop) per
@@ -809,6 +834,14 @@ def run(args, world, rank, local):
                    "frac": round(tflops / vpk, 4), "measured_issue_TFLOPs": VALU_MEASURED_TFLOPS[dtype],
                    "floor_ms": {"hbm": round(hbm_floor, 5), "valu": round(valu_floor, 5)}}
         roof["compute"] = compute
+        if iso:
+            roof["isolated"] = {
+                "method": "each pass timed alone (its launches back to back over the rotated buffer sets, HIP event "
+                          "nodes, one context); in the step the inverse also carries the drain of the forward's "
+                          "write-back coefficient rows",
+                "ms_per_launch": {f: round(v, 5) for f, v in iso.items()},
+                "achieved_GBps": {f: round(pass_bytes[f] / (v * 1e-3) / 1e9, 1) for f, v in iso.items()},
+                "frac": {f: round(pass_bytes[f] / (v * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) for f, v in iso.items()}}
         if valu_floor > hbm_floor:
             # VALU-bound pass: the headline roofline fields carry the compute roof; the HBM figures stay
             # beside them

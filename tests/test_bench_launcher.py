@@ -116,7 +116,7 @@ def test_no_collective_inside_timed_interval():
         def __init__(self):
             self.eng, self.stream = Eng(), Stream()
 
-        def step_fn(self, flags):
+        def step_fn(self, flags, only=None):
             return lambda i=0: log.append("step")
 
     class Wl:
@@ -144,3 +144,28 @@ def test_no_collective_inside_timed_interval():
     assert window.count("replay") == 2   # one K-step graph per context
     assert "barrier" in log[:i0] and "barrier" in log[i1:]   # contract barriers, both outside
     assert dev_s == pytest.approx(1e-3)
+
+
+def test_schedule_policy_per_shape():
+    # bench.plan_schedule (round 5): the 8-GPU shard of the headline (512 rows) pipelines consecutive steps,
+    # the full 4096-row batch splits over 4 contexts, long signals keep sequential steps / 2 contexts; the
+    # weak-scaling pass plans its own -- rows and N decide, not the strong-scaling shard
+    import argparse
+    import bench
+    a = argparse.Namespace(contexts=0, rotate=0, rotate_outputs=False, overlap_steps=False)
+    cus = 256
+    K, ov, rot = bench.plan_schedule(a, 512, 4096, 8, cus, "fwd+inv")
+    assert ov and K == 1 and rot[0] >= 2 and rot[1]
+    K, ov, rot = bench.plan_schedule(a, 4096, 4096, 8, cus, "fwd+inv")
+    assert not ov and K == 4 and rot[0] * 4096 * 4096 * 8 >= 512 << 20
+    K, ov, _ = bench.plan_schedule(a, 256, 1 << 20, 8, cus, "fwd+inv")          # db8-stream
+    assert not ov and K == 1
+    K, ov, _ = bench.plan_schedule(a, 16384, 16384, 8, cus, "denoise")         # sym8-denoise
+    assert not ov and K == 2
+    K, ov, _ = bench.plan_schedule(a, 65536, 8192, 4, cus, "fwd+inv")          # coif5-f32
+    assert not ov and K == 2
+    K, ov, _ = bench.plan_schedule(a, 1024, 4096, 8, cus, "fwd+inv")
+    assert not ov and K == 2
+    a.contexts = 3
+    K, ov, _ = bench.plan_schedule(a, 512, 4096, 8, cus, "fwd+inv")
+    assert not ov and K == 3

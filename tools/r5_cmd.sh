@@ -1,7 +1,7 @@
-# round-5: compile-time tap offsets in the deep forward (VW_DEEP_CK) and the inverse multi-level tiles (VW_MULTI_CK)
-# -- parity on the product build, then same-box A/B: ck0 (both runtime), mck0 (deep only), ck1 (both)
+# round-5: noise sigma with merged block reductions, 4 vs 8 waves per SIMD -- parity (denoise, medians,
+# config 3), then same-box A/B on sym8-denoise against the round-4 kernels (ck0)
 set -u
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
-bash tools/gpu_steps.sh t:test_gpu_deep.py t:config4 t:multilevel || exit $?
-export AB_ck_V="VW_LIB_PATH=vwvar/var_ck0/libvectorwave_amd.so|;VW_LIB_PATH=vwvar/var_mck0/libvectorwave_amd.so|;VW_LIB_PATH=vwvar/var_ck1/libvectorwave_amd.so|" AB_ck_STEPS=10 AB_ck_REPS=3 AB_ck_CFG=db8-stream
-bash tools/gpu_steps.sh ab:ck
+bash tools/gpu_steps.sh t:test_gpu_denoiser.py t:config3 t:median t:sigma || exit $?
+export AB_sg_V="VW_LIB_PATH=vwvar/var_ck0/libvectorwave_amd.so|;VW_LIB_PATH=vwvar/var_sw4/libvectorwave_amd.so|;VW_LIB_PATH=vwvar/var_sw8/libvectorwave_amd.so|" AB_sg_STEPS=10 AB_sg_REPS=3 AB_sg_CFG=sym8-denoise
+bash tools/gpu_steps.sh ab:sg
