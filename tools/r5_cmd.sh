@@ -1,7 +1,6 @@
-# round-5: contexts per GPU for the long-signal configs (schedule policy check)
+# round-5: deep forward output pairs (VW_DEEP_PAIR) -- parity on the product build, same-box A/B on db8-stream
 set -u
 cd "${GRAFT_REPO_ROOT:-.}" || exit 2
-export AB_c8_V="|;|--contexts 2;|--contexts 4" AB_c8_STEPS=10 AB_c8_REPS=2 AB_c8_CFG=db8-stream
-export AB_cs_V="|;|--contexts 1;|--contexts 4" AB_cs_STEPS=10 AB_cs_REPS=2 AB_cs_CFG=sym8-denoise
-export AB_cc_V="|;|--contexts 4" AB_cc_STEPS=10 AB_cc_REPS=2 AB_cc_CFG=coif5-f32
-bash tools/gpu_steps.sh ab:c8 ab:cs ab:cc
+bash tools/gpu_steps.sh t:test_gpu_deep.py t:config4 || exit $?
+export AB_pr_V="VW_LIB_PATH=vwvar/var_pair0/libvectorwave_amd.so|;VW_LIB_PATH=vwvar/var_pair1/libvectorwave_amd.so|" AB_pr_STEPS=10 AB_pr_REPS=3 AB_pr_CFG=db8-stream
+bash tools/gpu_steps.sh ab:pr

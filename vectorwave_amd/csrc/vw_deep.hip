@@ -52,6 +52,9 @@ constexpr int kDeepThreads = 256;
 #define VW_DEEP_TC 8   // taps whose LDS reads the no-wrap forward loop issues before their FMAs
 #endif
 constexpr int kDeepTC = VW_DEEP_TC;
+#ifndef VW_DEEP_PAIR
+#define VW_DEEP_PAIR 1  // forward levels with spacing >= 4: output pairs P0, P0 + SK share their reads
+#endif
 
 
 // One wave's LDS-DMA of 16 positions x 64 bytes (1 KiB): lane -> position lane / 4, 16-byte chunk lane % 4.
@@ -166,95 +169,119 @@ __global__ void __launch_bounds__(kDeepThreads) k_forward_deep(const DeepArgs<T>
     if (t + pf.D < nt) dma_tile(u0 + pf.D * kDeepT);  // ring 0: tile t + D, in flight across D tiles
     const bool store = u0 >= p.warm;                   // tile-uniform; the last tile's tail is masked
     const int q0 = q_tile(u0);
-    long long gofs[NP];
-    bool live[NP];
-#pragma unroll
-    for (int r = 0; r < NP; ++r) {
-      gofs[r] = rowoff + (long long)qwrap(q0 + pi + 64 * r) * P + ce;
-      live[r] = store && u0 + pi + 64 * r < total;
-    }
     for (int k = 0; k < g; ++k) {
       if (k > 0) lds_barrier();  // ring k holds level k-1's approximation of this tile
       const int cap = p.cap[k], sk = 1 << k;
       const T* ring = lds + p.off[k] + ce;
       const int s0 = u0 % cap;
-      int br[NP];
+      // One level of this tile.  KC >= 0: compile-time spacing 2^KC (immediate LDS offsets); -1: runtime.
+      auto level = [&](auto kc) __attribute__((always_inline)) {
+        constexpr int KC = decltype(kc)::value;
+        // Output pairs (spacing SK >= 4, VW_DEEP_PAIR): a thread's two positions are P0 and P0 + SK, so
+        // they share L - 1 of their inputs -- L + 1 LDS reads instead of 2L.  Consecutive threads take
+        // consecutive residues of the block (P0 = (pi / SK) * 2SK + pi % SK), so a quarter-wave still
+        // reads four consecutive positions (256 contiguous bytes, conflict-free).  Below SK = 4 that
+        // mapping would put two lanes of a quarter-wave on one bank group: those levels keep pi, pi + 64.
+        constexpr bool PAIR = VW_DEEP_PAIR && KC >= 2;
+        constexpr int KP = PAIR ? KC : 0;
+        int pos[NP];
 #pragma unroll
-      for (int r = 0; r < NP; ++r) {
-        const int v = s0 + pi + 64 * r;
-        br[r] = v >= cap ? v - cap : v;
-      }
-      T al[NP][V], ah[NP][V];
-#pragma unroll
-      for (int r = 0; r < NP; ++r)
-#pragma unroll
-        for (int e = 0; e < V; ++e) { al[r][e] = T(0); ah[r][e] = T(0); }
-      // tap i reads slot br - i*sk (mod cap), i ascending; the products are the same in every form below
-      auto fma2 = [&](int r, int i, const vec& x) __attribute__((always_inline)) {
-#pragma unroll
-        for (int e = 0; e < V; ++e) {
-          al[r][e] = madd<FMA>(al[r][e], x[e], p.lo[i]);
-          ah[r][e] = madd<FMA>(ah[r][e], x[e], p.hi[i]);
-        }
-      };
-      // Compile-time spacing (the first kDeepCK levels of a group): the reads of a lane sit at fixed
-      // distances (L-1-i)*SK positions above a0 = slot br - (L-1)*SK, so each is ONE ds_read at an
-      // immediate offset from a0 -- or from a1 = a0 + cap where that slot wrapped (br < i*SK: one compare
-      // and select per read).  A wave whose lanes never wrap at this level takes the select-free loop.
-      // The runtime form (wrap arithmetic per read: sub, compare, select, address) measured ~1 INT32 VALU
-      // per FMA on db8-stream's levels 6..10 (profiles/r05/pmc_mix_db8_a0b973e.txt).
-      auto taps_c = [&](auto kc) __attribute__((always_inline)) {
-        constexpr int SK = 1 << decltype(kc)::value;
-        const T* a0[NP];
-        const T* a1[NP];
-        bool nowrap = true;
+        for (int r = 0; r < NP; ++r)
+          pos[r] = PAIR ? ((pi >> KP) << (KP + 1)) + (pi & ((1 << KP) - 1)) + (r << KP) : pi + 64 * r;
+        int br[NP];
 #pragma unroll
         for (int r = 0; r < NP; ++r) {
-          a0[r] = ring + (br[r] - (L - 1) * SK) * C;
-          a1[r] = a0[r] + cap * C;
-          nowrap = nowrap && br[r] >= (L - 1) * SK;
+          const int v = s0 + pos[r];
+          br[r] = v >= cap ? v - cap : v;
         }
-        if (__all(nowrap)) {
-          // 32-bit LDS base per lane, laundered so the compiler keeps it (and the positive immediate
-          // offsets) instead of re-basing on the highest tap with negative adds; the reads of a chunk of
-          // kDeepTC taps are issued together (VGPRs to spare at two workgroups per CU), then its FMAs
-          unsigned ab[NP];
+        T al[NP][V], ah[NP][V];
+#pragma unroll
+        for (int r = 0; r < NP; ++r)
+#pragma unroll
+          for (int e = 0; e < V; ++e) { al[r][e] = T(0); ah[r][e] = T(0); }
+        // tap i of output r reads slot br[r] - i*sk (mod cap), i ascending; the same products in every form
+        auto fma2 = [&](int r, int i, const vec& x) __attribute__((always_inline)) {
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            al[r][e] = madd<FMA>(al[r][e], x[e], p.lo[i]);
+            ah[r][e] = madd<FMA>(ah[r][e], x[e], p.hi[i]);
+          }
+        };
+        if constexpr (PAIR) {
+          // reads t = 0..L at slot br[1] - t*SK: tap t of P0 + SK (t < L), tap t - 1 of P0 (t >= 1)
+          constexpr int SK = 1 << KP;
+          const T* a0 = ring + (br[1] - L * SK) * C;
+          const T* a1 = a0 + cap * C;
+          auto use = [&](int t, const vec& x) __attribute__((always_inline)) {
+            if (t < L) fma2(1, t, x);
+            if (t >= 1) fma2(0, t - 1, x);
+          };
+          if (__all(br[1] >= L * SK)) {
+            const unsigned ab = lds_base(a0);
+            static_for<0, (L + 1 + kDeepTC - 1) / kDeepTC>([&](auto c) __attribute__((always_inline)) {
+              constexpr int T0 = decltype(c)::value * kDeepTC;
+              constexpr int T1 = (T0 + kDeepTC < L + 1) ? T0 + kDeepTC : L + 1;
+              vec xs[T1 - T0];
+#pragma unroll
+              for (int t = T0; t < T1; ++t)
+                xs[t - T0] = lds_vec_at<vec>(ab + (unsigned)((L - t) * SK * C * (int)sizeof(T)));
+#pragma unroll
+              for (int t = T0; t < T1; ++t) use(t, xs[t - T0]);
+            });
+          } else {
+#pragma unroll
+            for (int t = 0; t <= L; ++t) {
+              const T* a = br[1] >= t * SK ? a0 : a1;
+              use(t, *reinterpret_cast<const vec*>(a + (L - t) * SK * C));
+            }
+          }
+        } else if constexpr (KC >= 0) {
+          // Compile-time spacing: the reads of a lane sit at fixed distances (L-1-i)*SK positions above
+          // a0 = slot br - (L-1)*SK, so each is ONE ds_read at an immediate offset from a0 -- or from
+          // a1 = a0 + cap where that slot wrapped (br < i*SK: one compare and select per read).  A wave
+          // whose lanes never wrap at this level takes the select-free loop.  The runtime form (wrap
+          // arithmetic per read: sub, compare, select, address) measured ~1 INT32 VALU per FMA on
+          // db8-stream's levels 6..10 (profiles/r05/pmc_mix_db8_a0b973e.txt).
+          constexpr int SK = 1 << (KC >= 0 ? KC : 0);
+          const T* a0[NP];
+          const T* a1[NP];
+          bool nowrap = true;
 #pragma unroll
           for (int r = 0; r < NP; ++r) {
-            ab[r] = (unsigned)(uintptr_t)a0[r];
-            asm volatile("" : "+v"(ab[r]));
+            a0[r] = ring + (br[r] - (L - 1) * SK) * C;
+            a1[r] = a0[r] + cap * C;
+            nowrap = nowrap && br[r] >= (L - 1) * SK;
           }
-          static_for<0, (L + kDeepTC - 1) / kDeepTC>([&](auto c) __attribute__((always_inline)) {
-            constexpr int I0 = decltype(c)::value * kDeepTC;
-            constexpr int I1 = (I0 + kDeepTC < L) ? I0 + kDeepTC : L;
-            vec xs[I1 - I0][NP];
+          if (__all(nowrap)) {
+            // 32-bit LDS base per lane (laundered: the immediate offsets stay positive); the reads of a
+            // chunk of kDeepTC taps are issued together (VGPRs to spare at two workgroups per CU)
+            unsigned ab[NP];
 #pragma unroll
-            for (int i = I0; i < I1; ++i)
+            for (int r = 0; r < NP; ++r) ab[r] = lds_base(a0[r]);
+            static_for<0, (L + kDeepTC - 1) / kDeepTC>([&](auto c) __attribute__((always_inline)) {
+              constexpr int I0 = decltype(c)::value * kDeepTC;
+              constexpr int I1 = (I0 + kDeepTC < L) ? I0 + kDeepTC : L;
+              vec xs[I1 - I0][NP];
 #pragma unroll
-              for (int r = 0; r < NP; ++r)
-                xs[i - I0][r] = lds_vec_at<vec>(ab[r] + (unsigned)((L - 1 - i) * SK * C * (int)sizeof(T)));
+              for (int i = I0; i < I1; ++i)
 #pragma unroll
-            for (int i = I0; i < I1; ++i)
+                for (int r = 0; r < NP; ++r)
+                  xs[i - I0][r] = lds_vec_at<vec>(ab[r] + (unsigned)((L - 1 - i) * SK * C * (int)sizeof(T)));
 #pragma unroll
-              for (int r = 0; r < NP; ++r) fma2(r, i, xs[i - I0][r]);
-          });
+              for (int i = I0; i < I1; ++i)
+#pragma unroll
+                for (int r = 0; r < NP; ++r) fma2(r, i, xs[i - I0][r]);
+            });
+          } else {
+#pragma unroll
+            for (int i = 0; i < L; ++i)
+#pragma unroll
+              for (int r = 0; r < NP; ++r) {
+                const T* a = br[r] >= i * SK ? a0[r] : a1[r];
+                fma2(r, i, *reinterpret_cast<const vec*>(a + (L - 1 - i) * SK * C));
+              }
+          }
         } else {
-#pragma unroll
-          for (int i = 0; i < L; ++i)
-#pragma unroll
-            for (int r = 0; r < NP; ++r) {
-              const T* a = br[r] >= i * SK ? a0[r] : a1[r];
-              fma2(r, i, *reinterpret_cast<const vec*>(a + (L - 1 - i) * SK * C));
-            }
-        }
-      };
-      switch (VW_DEEP_CK ? k : -1) {
-        case 0: taps_c(std::integral_constant<int, 0>{}); break;
-        case 1: taps_c(std::integral_constant<int, 1>{}); break;
-        case 2: taps_c(std::integral_constant<int, 2>{}); break;
-        case 3: taps_c(std::integral_constant<int, 3>{}); break;
-        case 4: taps_c(std::integral_constant<int, 4>{}); break;
-        default:
 #pragma unroll
           for (int i = 0; i < L; ++i) {
 #pragma unroll
@@ -264,29 +291,40 @@ __global__ void __launch_bounds__(kDeepThreads) k_forward_deep(const DeepArgs<T>
               fma2(r, i, *reinterpret_cast<const vec*>(ring + sl * C));
             }
           }
-          break;
-      }
-#pragma unroll
-      for (int r = 0; r < NP; ++r)
-#pragma unroll
-        for (int e = 0; e < V; ++e) {  // both chains computed here, not sunk into the store branch
-          asm volatile("" : "+v"(al[r][e]));
-          asm volatile("" : "+v"(ah[r][e]));
         }
-      const int cap1 = k + 1 < g ? p.cap[k + 1] : 1;
-      const int s1 = u0 % cap1;
 #pragma unroll
-      for (int r = 0; r < NP; ++r) {
-        vec od, oa;
+        for (int r = 0; r < NP; ++r)
 #pragma unroll
-        for (int e = 0; e < V; ++e) { od[e] = ah[r][e]; oa[e] = al[r][e]; }
-        if (live[r]) deep_store<vec>(p.out_d[k] + gofs[r], od);
-        if (k + 1 < g) {
-          const int v = s1 + pi + 64 * r;
-          *reinterpret_cast<vec*>(lds + p.off[k + 1] + (v >= cap1 ? v - cap1 : v) * C + ce) = oa;
-        } else if (live[r]) {
-          deep_store<vec>(p.out + gofs[r], oa);
+          for (int e = 0; e < V; ++e) {  // both chains computed here, not sunk into the store branch
+            asm volatile("" : "+v"(al[r][e]));
+            asm volatile("" : "+v"(ah[r][e]));
+          }
+        const int cap1 = k + 1 < g ? p.cap[k + 1] : 1;
+        const int s1 = u0 % cap1;
+#pragma unroll
+        for (int r = 0; r < NP; ++r) {
+          vec od, oa;
+#pragma unroll
+          for (int e = 0; e < V; ++e) { od[e] = ah[r][e]; oa[e] = al[r][e]; }
+          // every tile issues the same number of stores per wave (DeepPf); only the last tile's tail is masked
+          const bool live = store && u0 + pos[r] < total;
+          const long long gofs = rowoff + (long long)qwrap(q0 + pos[r]) * P + ce;
+          if (live) deep_store<vec>(p.out_d[k] + gofs, od);
+          if (k + 1 < g) {
+            const int v = s1 + pos[r];
+            *reinterpret_cast<vec*>(lds + p.off[k + 1] + (v >= cap1 ? v - cap1 : v) * C + ce) = oa;
+          } else if (live) {
+            deep_store<vec>(p.out + gofs, oa);
+          }
         }
+      };
+      switch (VW_DEEP_CK ? k : -1) {
+        case 0: level(std::integral_constant<int, 0>{}); break;
+        case 1: level(std::integral_constant<int, 1>{}); break;
+        case 2: level(std::integral_constant<int, 2>{}); break;
+        case 3: level(std::integral_constant<int, 3>{}); break;
+        case 4: level(std::integral_constant<int, 4>{}); break;
+        default: level(std::integral_constant<int, -1>{}); break;
       }
     }
     // tile t+1's batch has landed once at most the operations issued after it are outstanding
