@@ -435,12 +435,14 @@ def test_multilevel_tiles_bit_exact(engine, tile):
 
 
 @pytest.mark.parametrize("opts", [dict(VW_MULTI_PAD=0), dict(VW_MULTI_INV_TILE=1792), dict(VW_MULTI_INV_TILE=1024),
-                                  dict(VW_MULTI_INV_TILE=512, VW_MULTI_TILE=512)],
+                                  dict(VW_MULTI_INV_TILE=512, VW_MULTI_TILE=512), dict(VW_MULTI_NI=4),
+                                  dict(VW_MULTI_NI=4, VW_MULTI_TILE=1024), dict(VW_MULTI_NI=8)],
                          ids=lambda d: ",".join(f"{k}={v}" for k, v in d.items()))
 def test_multilevel_inverse_padded_layout(engine, opts):
-    """k_inverse_multi's padded LDS layout at the register-blocked levels (VW_MULTI_PAD, default on) and
-    its own tile (VW_MULTI_INV_TILE): EXACT bit-exact vs the restatement; FMA and fp32 identical bits
-    to the default configuration (the same per-output operation sequence, only LDS addresses move)."""
+    """k_inverse_multi's padded LDS layout at the register-blocked levels (VW_MULTI_PAD, default on), its own
+    tile (VW_MULTI_INV_TILE) and its outputs per thread (VW_MULTI_NI: 8, or 4 on the largest tile whose levels
+    fit, with the NV = 4 pad layouts): EXACT bit-exact vs the restatement; FMA and fp32 identical bits to the
+    default configuration (the same per-output operation sequence, only LDS addresses move)."""
     import torch
     with engine.options(VW_FORCE_TILED=1):
         for w, n, J in [(Daubechies.DB8, 1 << 15, 9), (Daubechies.DB4, 12288, 8), (Symlet.SYM8, 1 << 14, 6)]:

@@ -82,6 +82,9 @@ struct Tuning {
   int multi_pf = 1;        // VW_MULTI_PF: k_inverse_multi prefetches the next detail tile
   int multi_pad = 1;       // VW_MULTI_PAD: k_inverse_multi's padded LDS layout at register-blocked levels
   int multi_inv_tile = 0;  // VW_MULTI_INV_TILE: k_inverse_multi's tile (0 = VW_MULTI_TILE's)
+  int multi_ni = 4;        // VW_MULTI_NI: k_inverse_multi's output vectors per thread -- 4 (fp64, on the largest tile
+                           // whose levels fit 256 threads) or 8; db8-stream inverse 9.19-9.33 -> 8.75-8.80 ms
+                           // (profiles/r05/ab_db8_inverse_multi_ni4.log)
   bool no_sweep = false;   // VW_NO_SWEEP: no column sweeps for deep levels
   int sweep_qc = kSweepChunk;  // VW_SWEEP_QC: q-chunk per sweep thread
   int unroll_max = kMaxTaps;   // VW_UNROLL_MAX: longest filter that runs the tap-unrolled fused kernels
@@ -127,6 +130,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_MULTI_PF") t.multi_pf = v < 0 ? d.multi_pf : v;
   else if (k == "VW_MULTI_PAD") t.multi_pad = v < 0 ? d.multi_pad : v;
   else if (k == "VW_MULTI_INV_TILE") t.multi_inv_tile = v < 0 ? 0 : v;
+  else if (k == "VW_MULTI_NI") t.multi_ni = v < 0 ? d.multi_ni : v == 4 ? 4 : 8;
   else if (k == "VW_NO_SWEEP") t.no_sweep = v > 0;
   else if (k == "VW_SWEEP_QC") t.sweep_qc = v >= 16 ? v : d.sweep_qc;
   else if (k == "VW_UNROLL_MAX") t.unroll_max = v < 0 ? d.unroll_max : v;
@@ -155,7 +159,7 @@ static const char* const kTuningKeys[] = {
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
     "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8",
-    "VW_DMA_NT"};
+    "VW_DMA_NT", "VW_MULTI_NI"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -1580,6 +1584,31 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         }
         // slack past D for the compile-time-stride reads (vw_device.h k_inverse_multi): 15*M <= 120 vectors
         m.slack = 160;
+        m.ni = kMultiInvNI;
+        // four output vectors per thread (fp64, padded layouts): at NI = 8 a 2048-sample tile gives the
+        // register-blocked levels 129-144 threads of work, i.e. 2.0-2.3 of the workgroup's 4 waves (one SIMD idle,
+        // one mostly idle); at NI = 4 on the largest tile whose levels fit 256 threads (1792 for db8) all four
+        // waves work.  The group itself stays as planned above.
+        if (tu.multi_ni == 4 && sizeof(T) == 8 && m.pad) {
+          auto fits = [&](int64_t t) {
+            if ((t + m.ext[g - 1]) / V > (int64_t)kMultiPF * 256) return false;
+            for (int k = 0; k < g; ++k) {
+              const int64_t s = lv[j0 - 1 + k].s, M = s % V == 0 ? s / V : 0;
+              const int64_t nv = (t + (k > 0 ? m.ext[k - 1] : 0)) / V;
+              const bool blk = M == 1 || M == 2 || M == 4 || M == 8;
+              if (blk ? (nv + 4 * M - 1) / (4 * M) * M > 256 : nv > 4 * 256) return false;
+            }
+            return true;
+          };
+          int64_t t = mtile;
+          while (t >= 512 && !fits(t)) t -= 64 * V;
+          if (t >= 512) {
+            m.ni = 4;
+            m.tile = (int)t;
+            const int nvmax = (int)((t + m.ext[g - 1]) / V) + 1;
+            m.region = (nvmax + nvmax / 4 + 1) * V;  // layouts 2 / 3 add at most u/4
+          }
+        }
         copy_taps(m.lo, lo, L);
         copy_taps(m.hi, hi, L);
         LaunchTimer lt(c, "inverse_level");

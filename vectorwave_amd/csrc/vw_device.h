@@ -2316,15 +2316,17 @@ __global__ void __launch_bounds__(256) k_forward_multi(const MultiArgs<T> p) {
 }
 
 // Inverse: A = a_j, D = d_j (thresholded on load for denoise); a_{j-1} is computed into registers
-// (kMultiInvNI vectors per thread) and written over A after a barrier -- two LDS regions, so four
-// 256-thread workgroups fit a CU (a third region for a_{j-1} measured 1.2x slower: two per CU).
+// (NI vectors per thread) and written over A after a barrier -- two LDS regions, so three 256-thread
+// workgroups fit a CU (a third region for a_{j-1} measured 1.2x slower: two per CU).  NI = 4 (fp64, host
+// policy) on a tile whose register-blocked levels give all four waves work: at NI = 8 a 2048-sample db8
+// tile had 129-144 threads of work per level, one SIMD idle and one mostly idle.
 #ifndef VW_MULTI_CK
 #define VW_MULTI_CK 1  // k_inverse_multi register-blocked levels: compile-time strides, immediate LDS offsets
 #endif
-template <typename T, int L, bool FMA>
+template <typename T, int L, bool FMA, int NI = kMultiInvNI>
 __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
   constexpr int V = VT<T>::V;
-  constexpr int NI = kMultiInvNI;  // host contract: (tile + ext[top]) / V <= NI * 256
+  static_assert(NI == 8 || NI == 4, "outputs per thread");  // host contract: every level's blocks fit 256 threads
   using vec = typename VT<T>::v;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   T* const A = reinterpret_cast<T*>(smem);  // positions [0, span + ext[k])
@@ -2345,13 +2347,27 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
   // Padded LDS layout (p.pad, host contract: pf and rblk on): the register-blocked levels (vector
   // stride m = s/V in 1..8) read lanes NI*m vectors apart -- an 8-way bank conflict at m = 1 in the
   // natural layout (62 % of LDS cycles in conflicts on db8 levels 1-5, profiles/r03/pmc_db8_stream.txt).
-  // Level k's A and D then hold logical vector u at u + u/8 (blk_layout's NV = 8 layout: conflict-free
-  // ds_read_b128 at every m <= 8); levels with m = 0 or m >= 16 keep the natural layout.
-  auto padded = [&](int k) {
-    const int sk = p.s0 << k;
-    return p.pad != 0 && sk >= V && sk % V == 0 && sk / V < 16;
+  // Level k's A and D then hold logical vector u at u + u/8 at NI = 8 (layout 1), at NI = 4 at u + u/4
+  // (m <= 4, layout 2) or u + 2*(u/8) (m = 8, layout 3) -- blk_layout's NV = 8 / NV = 4 layouts, conflict-free
+  // ds_read_b128 at every m <= 8 under the gfx950 lane groups; levels with m = 0 or m >= 16 keep the natural
+  // layout (0).
+  // (a layout is (shift, pad): u -> u + (u >> shift) * pad -- one formula, no per-layout copies of the
+  // hoisted store addresses)
+  auto layout = [&](int k) {
+    const int sk = p.s0 << k, m = sk / V;
+    int2 lay = make_int2(30, 0);
+    if (p.pad != 0 && sk >= V && sk % V == 0) {
+      if constexpr (NI >= 8) {
+        if (m < 16) lay = make_int2(3, 1);
+      } else {
+        if (m <= 4) lay = make_int2(2, 1);
+        else if (m == 8) lay = make_int2(3, 2);
+      }
+    }
+    return lay;
   };
-  auto phys = [&](int u, bool pd) { return pd ? u + (u >> 3) : u; };
+  auto padded = [](int2 lay) { return lay.y != 0; };
+  auto phys = [](int u, int2 lay) { return u + (u >> lay.x) * lay.y; };
   vec dreg[kMultiPF];
   auto d_load = [&](int k) {
     const T* sd = p.src_d[k];
@@ -2369,7 +2385,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
     }
   };
   auto d_store = [&](int k) {
-    const bool pd = padded(k);
+    const int2 pd = layout(k);
     const T* th = p.thr[k];
     const T thb = th ? th[b] : T(0);
     const int nvd = (span + p.ext[k]) / V;
@@ -2387,7 +2403,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
   };
   if (p.pad) {
     // a_top through registers into level top's layout (the d_load path, no threshold)
-    const bool pd = padded(top);
+    const int2 pd = layout(top);
     const int nva = (span + p.ext[top]) / V;
 #pragma unroll
     for (int i = 0; i < kMultiPF; ++i) {
@@ -2435,26 +2451,30 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
         const int pr = threadIdx.x;
         const int vb = (pr / m) * m * NI + pr % m;
         const int lim = (span + p.ext[k]) / V - 1;  // last vector of the A/D regions
-        const bool pdk = padded(k), pdn = k > 0 && padded(k - 1);
+        const int2 pdk = layout(k), pdn = k > 0 ? layout(k - 1) : make_int2(30, 0);
 #pragma unroll
         for (int r = 0; r < NI; ++r)
 #pragma unroll
           for (int e = 0; e < V; ++e) acc[r][e] = T(0);
         if (pr < pairs) {
-          // compile-time stride M (padded iff PD): the reads of a lane sit at fixed offsets off(j) from
-          // phys(vb) -- (vb & 7) + (M*j & 7) < 8 for every M <= 8 here (vb % 8 = pr % M < M, NI = 8), so
-          // (vb + M*j) >> 3 = (vb >> 3) + (M*j >> 3) -- and each is one ds_read at an immediate offset.
+          // compile-time stride M and layout LC: the reads of a lane sit at fixed offsets off(j) from
+          // phys(vb) -- with G = 8 (layouts 1, 3) or 4 (layout 2) vectors per pad group, (vb % G) + (M*j % G) < G
+          // for every M <= 8 here (vb % G = pr % M < M, or M*j % G = 0), so (vb + M*j) / G = vb / G + M*j / G --
+          // and each is one ds_read at an immediate offset.
           // Reads past the region end (at most 15*M vectors, only for outputs that are never stored) stay
           // inside the allocation: the host adds p.slack >= 16*8 + 16 vectors after D (M <= 8 here).
           const T* const tlo = p.lo;
           const T* const thi = p.hi;
-          auto blk_c = [&](auto mc, auto pdc) __attribute__((always_inline)) {
+          auto blk_c = [&](auto mc, auto lc) __attribute__((always_inline)) {
             constexpr int M = decltype(mc)::value;
-            constexpr bool PD = decltype(pdc)::value;
-            constexpr auto off = [](int j) { return PD ? M * j + ((M * j) >> 3) : M * j; };
+            constexpr int PD = decltype(lc)::value;
+            constexpr auto off = [](int j) {
+              return PD == 1 ? M * j + ((M * j) >> 3) : PD == 2 ? M * j + ((M * j) >> 2) : M * j + (((M * j) >> 3) << 1);
+            };
 #pragma unroll
             for (int br = 0; br < 2; ++br) {
-              const unsigned ab = lds_base((br == 0 ? A : D) + phys(vb, PD) * V);
+              const unsigned ab = lds_base((br == 0 ? A : D) + phys(vb, PD == 1 ? make_int2(3, 1) : PD == 2 ? make_int2(2, 1)
+                                                                                        : make_int2(3, 2)) * V);
 #pragma unroll
               for (int j = 0; j < NI + L - 1; ++j) {
                 const vec x = lds_vec_at<vec>(ab + (unsigned)(off(j) * V * (int)sizeof(T)));
@@ -2477,15 +2497,16 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
           using I2 = std::integral_constant<int, 2>;
           using I4 = std::integral_constant<int, 4>;
           using I8 = std::integral_constant<int, 8>;
-          using BT = std::true_type;
+          using P1 = std::integral_constant<int, NI >= 8 ? 1 : 2>;  // layout of m = 1, 2, 4
+          using P8 = std::integral_constant<int, NI >= 8 ? 1 : 3>;  // layout of m = 8
           // padded layouts only (the default, p.pad): more instantiations in this function raised it from 160
           // VGPRs to 238 + 1.3 KiB of scratch (the taps, hoisted across the switch)
-          const int sel = VW_MULTI_CK && p.slack && pdk ? m : -1;
+          const int sel = VW_MULTI_CK && p.slack && padded(pdk) ? m : -1;
           switch (sel) {
-            case 1: blk_c(I1{}, BT{}); break;
-            case 2: blk_c(I2{}, BT{}); break;
-            case 4: blk_c(I4{}, BT{}); break;
-            case 8: blk_c(I8{}, BT{}); break;
+            case 1: blk_c(I1{}, P1{}); break;
+            case 2: blk_c(I2{}, P1{}); break;
+            case 4: blk_c(I4{}, P1{}); break;
+            case 8: blk_c(I8{}, P8{}); break;
             default:
 #pragma unroll
               for (int br = 0; br < 2; ++br) {
@@ -2543,7 +2564,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
     }
     if (k == 0) break;
     lds_barrier();  // every read of A and D done
-    const bool pdn = padded(k - 1);  // (this level itself is never padded: see padded())
+    const int2 pdn = layout(k - 1);  // (this level itself is never padded: see layout())
 #pragma unroll
     for (int i = 0; i < NI; ++i) {
       const int w = threadIdx.x + i * 256;

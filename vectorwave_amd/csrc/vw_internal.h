@@ -161,6 +161,7 @@ struct MultiArgs {
   int pf;                    // inverse: next level's detail tile prefetched into registers
   int pad;                   // inverse: padded LDS layout at the register-blocked levels (needs pf, rblk)
   int slack;                 // inverse: LDS vectors allocated past D (compile-time-stride reads, 0 = off)
+  int ni;                    // inverse: output vectors per thread, kMultiInvNI or 4 (fp64)
   T lo[kMaxTaps];
   T hi[kMaxTaps];
 };
