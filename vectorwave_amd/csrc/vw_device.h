@@ -1305,6 +1305,45 @@ __device__ __forceinline__ void blk_inv_branch_s(const T* Rb, int m, int sh, int
 #ifndef VW_BLK_SOFF
 #define VW_BLK_SOFF 1  // NV = 8 inverse branch: wave-uniform offsets where the layout allows (0: per-lane blk_phys)
 #endif
+#ifndef VW_BLK_CK8
+#define VW_BLK_CK8 1  // NV = 8 blocked inverse (FMA) at m = 1..64: immediate LDS offsets off one laundered base
+                      // (the same for k_forward_blk measured slower: forward 4.92-4.97 vs 4.78-4.85 ms, sym8)
+#endif
+
+// blk_inv_branch_c with the base laundered into a 32-bit LDS address (lds_base): every read is one
+// ds_read_b128 at an immediate offset -- no per-read scalar offset arithmetic (blk_inv_branch_s: four SALU
+// and one VALU per read) and no re-based 64-bit pointers.
+template <typename T, int L, bool FMA, int NV, int M, int TIGHT>
+__device__ __forceinline__ void blk_inv_branch_cl(const T* Rb, const T* f, T (&acc)[NV][VT<T>::V]) {
+  constexpr int V = VT<T>::V;
+  using vec = typename VT<T>::v;
+  using C = BlkC<M, NV, TIGHT>;
+  constexpr int TC = blk_chunk<T, NV>();
+  const unsigned ab = lds_base(Rb);
+  static_for<0, (L + TC - 1) / TC>([&](auto c) __attribute__((always_inline)) {
+    constexpr int I0 = decltype(c)::value * TC;
+    constexpr int I1 = (I0 + TC < L) ? I0 + TC : L;
+    T fc[I1 - I0];
+#pragma unroll
+    for (int i = I0; i < I1; ++i) fc[i - I0] = f[i];
+#pragma unroll
+    for (int q = I0; q < I1 + NV - 1; ++q) {
+      const vec x = lds_vec_at<vec>(ab + (unsigned)(C::off(q) * V * (int)sizeof(T)));
+#pragma unroll
+      for (int r = 0; r < NV; ++r) {
+        const int i = q - r;
+        if (i >= I0 && i < I1) {
+          vmadd<FMA>(acc[r], x, fc[i - I0]);
+        }
+      }
+      if (((q - I0) & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  });
+#pragma unroll
+  for (int r = 0; r < NV; ++r)
+#pragma unroll
+    for (int e = 0; e < V; ++e) asm volatile("" : "+v"(acc[r][e]));
+}
 
 // One inverse branch at vector stride m >= 1: the compile-time forms for m = 1..64 (immediate LDS
 // offsets stay below 64 KiB for L <= 30), the generic one otherwise.  Same reads, same sums.
@@ -1313,9 +1352,32 @@ __device__ __forceinline__ void blk_inv_any(const T* R, const BlkLayout& lo, int
                                             T (&acc)[NV][VT<T>::V]) {
   constexpr int V = VT<T>::V;
   if constexpr (NV >= 8) {
-    // compile-time forms measured slower at NV = 8 (sym8 fp64 inverse 7.18 -> 8.08 ms,
-    // profiles/r03/ab_sym8_cinv.log)
+    // compile-time forms through plain pointers measured slower at NV = 8 (sym8 fp64 inverse 7.18 -> 8.08 ms,
+    // profiles/r03/ab_sym8_cinv.log); off a laundered 32-bit base (blk_inv_branch_cl) they win: 6.32-6.38
+    // -> 6.17-6.28 ms (profiles/r05/ab_sym8_inverse_ck8.log)
     const int sh = __builtin_amdgcn_readfirstlane(lo.sh), pad = __builtin_amdgcn_readfirstlane(lo.pad);
+    if constexpr (VW_BLK_CK8 != 0 && FMA) {
+      // m = 1..64 where the pad group (8 vectors, or 16 in the tight layout) divides a thread's 8m-vector
+      // block (BlkC::ok) or there is none (m >= 16): the offset of vb + q*m from vb is the same for every
+      // lane.  FMA only: the EXACT kernel (mul + add per tap) spills 28 B/lane at its 128-VGPR cap with it.
+      const T* Rb = R + blk_phys(lo, vb) * V;
+      const int sel = (m == 1 || m == 2 || m == 4 || m == 8) && pad == 1 ? m * 2 + (tight ? 1 : 0)
+                      : (m == 16 || m == 32 || m == 64) && pad == 0 ? 4 * m : 0;
+      switch (sel) {
+        case 2: blk_inv_branch_cl<T, L, FMA, NV, 1, 0>(Rb, f, acc); return;
+        // (m = 1 in the tight layout: a thread's 8-vector block is half a 16-vector pad group -- per lane)
+        case 4: blk_inv_branch_cl<T, L, FMA, NV, 2, 0>(Rb, f, acc); return;
+        case 5: blk_inv_branch_cl<T, L, FMA, NV, 2, 1>(Rb, f, acc); return;
+        case 8: blk_inv_branch_cl<T, L, FMA, NV, 4, 0>(Rb, f, acc); return;
+        case 9: blk_inv_branch_cl<T, L, FMA, NV, 4, 1>(Rb, f, acc); return;
+        case 16: blk_inv_branch_cl<T, L, FMA, NV, 8, 0>(Rb, f, acc); return;
+        case 17: blk_inv_branch_cl<T, L, FMA, NV, 8, 1>(Rb, f, acc); return;
+        case 64: blk_inv_branch_cl<T, L, FMA, NV, 16, 0>(Rb, f, acc); return;   // m >= 16: natural layout
+        case 128: blk_inv_branch_cl<T, L, FMA, NV, 32, 0>(Rb, f, acc); return;
+        case 256: blk_inv_branch_cl<T, L, FMA, NV, 64, 0>(Rb, f, acc); return;
+        default: break;
+      }
+    }
     if (VW_BLK_SOFF && (pad == 0 || ((m * NV) & ((1 << sh) - 1)) == 0))
       blk_inv_branch_s<T, L, FMA, NV>(R + blk_phys(lo, vb) * V, m, sh, pad, f, acc);
     else
