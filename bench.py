@@ -1006,8 +1006,12 @@ def verify(torch, wl, w, J, pipeline, flags, nat):
     pr_bar = 1e-3 if wl.f32 else 1e-8   # truncated published taps (db8 J=10: ~1e-9; SURVEY.md key fact 5)
     ok = worst <= tol and (pr is None or pr < pr_bar)
     res = {"rows": rows, "max_abs_vs_oracle": worst, "tol": tol, "pr_max_abs": pr, "pr_bar": pr_bar, "ok": ok}
-    if not ok and os.environ.get("VW_BENCH_UNGUARDED") != "1":  # timing-only experiments: the line keeps ok false
-        raise RuntimeError(f"bench correctness guard failed: {res}")
+    if not ok:
+        if os.environ.get("VW_BENCH_UNGUARDED") != "1":
+            raise RuntimeError(f"bench correctness guard failed: {res}")
+        # timing-only experiments (variant builds that skip work by design, tools/ab.sh): the line is printed
+        # with ok false and marked, never as a result
+        res["unguarded_experiment"] = True
     return res
 
 
