@@ -1505,8 +1505,9 @@ __device__ __forceinline__ void blk_fwd_s(const T* Xb, int m, int sh, int pad, c
 
 // blk_fwd at a compile-time stride M (NV < 8, as blk_inv_branch_c): with the halo HLV a multiple of 16
 // vectors (host) the physical offset of logical vector vb + HLV + q*M from vb + HLV's is BlkC::off(q)
-// for every thread.  The reads run q = -(L-1) .. NV-1; they are addressed from the lowest one (Xq), so
-// every offset is a non-negative constant -- an immediate of the ds_read, no per-read address math.
+// for every thread.  The reads run q = -(L-1) .. NV-1; they are addressed from the lowest one, laundered
+// into a 32-bit LDS base (lds_base: through a plain pointer the compiler re-based most of them, 3 of 63 reads
+// per coif5 fp32 block kept an immediate), so every offset is a non-negative immediate of the ds_read.
 template <typename T, int L, bool FMA, int NV, int M>
 __device__ __forceinline__ void blk_fwd_c(const T* Xb, const T* flo, const T* fhi, T (&al)[NV][VT<T>::V],
                                           T (&ah)[NV][VT<T>::V]) {
@@ -1515,7 +1516,7 @@ __device__ __forceinline__ void blk_fwd_c(const T* Xb, const T* flo, const T* fh
   using C = BlkC<M, NV, 0>;
   constexpr int TC = blk_chunk<T, NV>();
   constexpr int QMIN = -(L - 1);
-  const T* const Xq = Xb + C::off(QMIN) * V;
+  const unsigned aq = lds_base(Xb + C::off(QMIN) * V);  // laundered: every read at an immediate offset
 #pragma unroll
   for (int r = 0; r < NV; ++r)
 #pragma unroll
@@ -1528,7 +1529,7 @@ __device__ __forceinline__ void blk_fwd_c(const T* Xb, const T* flo, const T* fh
     for (int i = I0; i < I1; ++i) { fl[i - I0] = flo[i]; fh[i - I0] = fhi[i]; }
 #pragma unroll
     for (int q = NV - 1 - I0; q > -I1; --q) {
-      const vec x = *reinterpret_cast<const vec*>(Xq + (C::off(q) - C::off(QMIN)) * V);
+      const vec x = lds_vec_at<vec>(aq + (unsigned)((C::off(q) - C::off(QMIN)) * V * (int)sizeof(T)));
 #pragma unroll
       for (int r = 0; r < NV; ++r) {
         const int i = r - q;
