@@ -466,6 +466,31 @@ def test_multilevel_inverse_padded_layout(engine, opts):
             assert torch.equal(y0, y1), (w.name(), dt)
 
 
+@pytest.mark.parametrize("ni", [4, 8])
+def test_multilevel_inverse_outputs_per_thread_edges(engine, ni):
+    """k_inverse_multi at NI = 4 (default for fp64: its own tile, 1792 samples for db8) and NI = 8 on the shapes
+    the tile choice touches: a partial last tile (N not a multiple of either tile), L = 30 (coif5: its reach moves
+    the NI = 4 tile down further), levels past the group (J = 8 at N = 16384, the deepest below the FFT region,
+    L_J <= N/8, where the reference switches to an FFT) and the SWT denoise thresholds applied on the detail
+    loads.  EXACT bit-exact vs the restatement."""
+    with engine.options(VW_FORCE_TILED=1, VW_MULTI_NI=ni):
+        for w, n, J in [(Daubechies.DB8, 3 * 1792 + 500, 5), (Coiflet.COIF5, 12000, 4), (Daubechies.DB8, 1 << 14, 8)]:
+            x = signals(2, n, 53)
+            tx = vw.MultiLevelMODWTTransform(w, vw.BoundaryMode.PERIODIC)
+            res = tx.decompose(x, J)
+            y = tx.reconstruct(res)
+            for b in range(2):
+                d, a = O.decompose(x[b], *lohi(w), O.PERIODIC, J)
+                exact(y[b], O.reconstruct(d, a, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC))
+        w, n, J = Daubechies.DB8, 9000, 5
+        x = signals(2, n, 59)
+        y, thr = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC).denoise(x, J, return_thresholds=True)
+        for b in range(2):
+            y_ref, t_ref = O.swt_denoise(x[b], *lohi(w), O.PERIODIC, J, wavelet_id=w.wavelet_id)
+            assert thr[b] == t_ref
+            exact(y[b], y_ref)
+
+
 # ---- alternative fused inverse kernels (selected by policy or option) ------------------------------------
 @pytest.mark.parametrize("opts", [dict(VW_INV_BUF=1), dict(VW_INV_BUF=2), dict(VW_NV=8), dict(VW_INV_BUF=1, VW_NV=8),
                                   dict(VW_INV_NV=2), dict(VW_INV_NV=2, VW_INV_BUF=1), dict(VW_INV_NV=2, VW_INV_BUF=2)],
