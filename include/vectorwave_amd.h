@@ -122,7 +122,18 @@ enum {
     VW_FLAG_BATCH_SYM_INVERSE = 1u << 6,
     /* Single-level forward: BatchSIMDMODWT.haarBatchMODWTSoA's hard-coded 0.5/-0.5 taps
      * (ext/extensions/modwt/BatchSIMDMODWT.java:86-140) when L == 2. */
-    VW_FLAG_BATCH_HAAR = 1u << 7
+    VW_FLAG_BATCH_HAAR = 1u << 7,
+    /* The unvalidated callers' non-finite semantics (multi-level calls without VW_FLAG_VALIDATE):
+     * the reference multiplies every tap of the upsampled filters, zeros included, so a NaN / +-Inf
+     * turns each output whose window reaches it through a zero tap into NaN (0 * Inf)
+     * -- BatchMODWT.multiLevelAoS (ext/extensions/modwt/BatchSIMDMODWT.java:384-424),
+     * inverseMultiLevelAoS -> MultiLevelMODWTTransform.reconstruct (core/modwt/MultiLevelMODWTTransform.java
+     * :339-349, :554-645), VectorWaveSwtAdapter.forwardParallel / inverse (core/swt/VectorWaveSwtAdapter.java
+     * :210-335, :435-487).  With this flag every row that holds a non-finite value in the call's inputs or
+     * outputs is recomputed with the reference's full-tap loops (exact arithmetic, also under
+     * VW_FLAG_FMA): NaN and +-Inf land exactly where the reference puts them.  Costs one extra read of
+     * the call's planes; streaming (vw_stream_*) ZERO / SYMMETRIC blocks are not covered. */
+    VW_FLAG_REF_NONFINITE = 1u << 8
 };
 
 /* ---- context ---------------------------------------------------------- */
@@ -144,6 +155,10 @@ VW_API int vw_ctx_device(vw_ctx *ctx);
 VW_API const char *vw_last_error(void);
 VW_API int64_t vw_last_error_index(void);
 VW_API const char *vw_version(void);
+/* Signal numbers in this thread's VW_ERR_NONFINITE messages count from `base`: a caller that splits one
+ * batch into row chunks (the JNI AoS natives, jni/vectorwave_amd_jni.c) sets each chunk's first row so the
+ * message names the batch's signal (AmdMultiLevelMODWT.decomposeBatch's contract); 0 restores. */
+VW_API void vw_set_signal_base(int64_t base);
 
 /* ---- bookkeeping (host only) ------------------------------------------ */
 /* getMaximumLevels(N) for a base filter of length L: largest J <= 9 with (L-1)*2^(J-1)+1 <= N. */
@@ -292,6 +307,8 @@ VW_API vw_status vw_stream_process_f64(vw_stream *s, const double *block, int64_
 VW_API vw_status vw_stream_flush_f64(vw_stream *s, int64_t tail_len, unsigned flags,
                                      double *details, double *approx);
 VW_API int64_t vw_stream_history_length(vw_stream *s, int level);
+/* Batch of the last processed block (the rows a flush emits); -1 before the first block. */
+VW_API int64_t vw_stream_batch(vw_stream *s);
 
 /* ---- captured steps ------------------------------------------------------- */
 /* A caller that repeats the same calls on the same buffers (a JNI server's per-batch loop, a

@@ -87,6 +87,18 @@ static int get_taps(JNIEnv *e, jdoubleArray a, Taps *t) {
 
 static size_t alen(JNIEnv *e, jdoubleArray a) { return a ? (size_t)(*e)->GetArrayLength(e, a) : 0; }
 
+/* A malformed Java argument found by the glue itself (a null row, a ragged row, a plane of the wrong
+ * length): throw IllegalArgumentException with its own message, so the Java caller never reads an
+ * unrelated vw_last_error() left by an earlier call.  The exception is pending when the native returns
+ * (Java throws it there; AmdNative.check is not reached). */
+static jint arg_error(JNIEnv *e, const char *msg) {
+  if (!(*e)->ExceptionCheck(e)) {
+    jclass k = (*e)->FindClass(e, "java/lang/IllegalArgumentException");
+    if (k) (*e)->ThrowNew(e, k, msg);
+  }
+  return VW_ERR_ARG;
+}
+
 /* ---- contexts ------------------------------------------------------------------------------ */
 JNIEXPORT jlong JNICALL VW_JNI(ctxCreate)(JNIEnv *e, jclass c, jint device) {
   (void)e; (void)c;
@@ -305,23 +317,26 @@ JNIEXPORT jint JNICALL VW_JNI(modwtInverseDirect)(JNIEnv *e, jclass c, jlong ctx
  * Java array's limit, e.g. 256 x 2^20 x 10 details) still goes through.  Row lengths are checked here
  * too (VW_ERR_ARG), the Java facade validates first with the reference's messages.  Local references
  * are released per row: the JNI guarantees only 16. */
-static const size_t kChunkBytes = (size_t)512 << 20;
+#ifndef VW_JNI_CHUNK_BYTES
+#define VW_JNI_CHUNK_BYTES ((size_t)512 << 20)  /* tests/jni_harness builds the glue with a few KiB */
+#endif
 
 static jsize chunk_rows(size_t per_row_doubles, jsize B) {
-  size_t r = kChunkBytes / (per_row_doubles * sizeof(double));
+  size_t r = (size_t)VW_JNI_CHUNK_BYTES / (per_row_doubles * sizeof(double));
   if (r < 1) r = 1;
   return r < (size_t)B ? (jsize)r : B;
 }
 
-/* rows[b0 .. b0+nb) (each of length n) <-> dst[nb][n]; 0 on a null row or a length mismatch */
+/* rows[b0 .. b0+nb) (each of length n) <-> dst[nb][n]; on a null row or a length mismatch: the
+ * IllegalArgumentException (arg_error), 0 returned */
 static int gather_rows(JNIEnv *e, jobjectArray rows, jsize b0, jsize nb, jsize n, double *dst) {
   for (jsize b = 0; b < nb; ++b) {
     jdoubleArray r = (jdoubleArray)(*e)->GetObjectArrayElement(e, rows, b0 + b);
-    if (!r) return 0;
+    if (!r) { arg_error(e, "all rows must be non-null"); return 0; }
     int ok = (*e)->GetArrayLength(e, r) == n;
     if (ok) (*e)->GetDoubleArrayRegion(e, r, 0, n, dst + (size_t)b * (size_t)n);
     (*e)->DeleteLocalRef(e, r);
-    if (!ok) return 0;
+    if (!ok) { arg_error(e, "all rows must have the same length"); return 0; }
   }
   return 1;
 }
@@ -329,11 +344,22 @@ static int gather_rows(JNIEnv *e, jobjectArray rows, jsize b0, jsize nb, jsize n
 static int scatter_rows(JNIEnv *e, jobjectArray rows, jsize b0, jsize nb, jsize n, const double *src) {
   for (jsize b = 0; b < nb; ++b) {
     jdoubleArray r = (jdoubleArray)(*e)->GetObjectArrayElement(e, rows, b0 + b);
-    if (!r) return 0;
+    if (!r) { arg_error(e, "output rows must be non-null"); return 0; }
     int ok = (*e)->GetArrayLength(e, r) == n;
     if (ok) (*e)->SetDoubleArrayRegion(e, r, 0, n, src + (size_t)b * (size_t)n);
     (*e)->DeleteLocalRef(e, r);
-    if (!ok) return 0;
+    if (!ok) { arg_error(e, "output rows must have the signal length"); return 0; }
+  }
+  return 1;
+}
+
+/* every plane of a double[][][] ([levels][batch][length]) non-null and of `batch` rows */
+static int planes_ok(JNIEnv *e, jobjectArray dpl, jsize levels, jsize batch) {
+  for (jsize l = 0; l < levels; ++l) {
+    jobjectArray pl = (jobjectArray)(*e)->GetObjectArrayElement(e, dpl, l);
+    const int ok = pl && (*e)->GetArrayLength(e, pl) == batch;
+    if (pl) (*e)->DeleteLocalRef(e, pl);
+    if (!ok) { arg_error(e, "detailPerLevel[L] must be non-null and length=batch for all L"); return 0; }
   }
   return 1;
 }
@@ -361,7 +387,9 @@ JNIEXPORT jint JNICALL VW_JNI(modwtForwardAoS)(JNIEnv *e, jclass c, jlong ctx, j
   if (!x || !details || !approx) return VW_ERR_NULL;
   const jsize B = (*e)->GetArrayLength(e, x), N = row_len(e, x);
   if (N < 1) return VW_ERR_EMPTY;
-  if ((*e)->GetArrayLength(e, details) != J || (*e)->GetArrayLength(e, approx) != B) return VW_ERR_ARG;
+  if ((*e)->GetArrayLength(e, details) != J) return arg_error(e, "details must hold one plane per level");
+  if ((*e)->GetArrayLength(e, approx) != B) return arg_error(e, "approx must hold one row per signal");
+  if (!planes_ok(e, details, J, B)) return VW_ERR_ARG;
   const jsize CB = chunk_rows((size_t)(J + 2) * (size_t)N, B);
   int oom = 0;
   double *px = out_buf(0, (size_t)CB * N, &oom), *pd = out_buf(1, (size_t)J * CB * N, &oom);
@@ -371,13 +399,15 @@ JNIEXPORT jint JNICALL VW_JNI(modwtForwardAoS)(JNIEnv *e, jclass c, jlong ctx, j
   for (jsize b0 = 0; b0 < B && st == VW_OK; b0 += CB) {
     const jsize nb = B - b0 < CB ? B - b0 : CB;
     if (!gather_rows(e, x, b0, nb, N, px)) { st = VW_ERR_ARG; break; }
+    vw_set_signal_base(b0);  /* a non-finite error names the batch's signal, not the chunk's */
     st = vw_modwt_forward_f64(CTX(ctx), px, nb, N, N, tl.v, th.v, tl.n, wid, boundary, J,
                               (unsigned)flags | HOST_FLAGS, pd, pa);
+    vw_set_signal_base(0);
     if (st != VW_OK) break;
     for (jsize l = 0; l < J && st == VW_OK; ++l) {
       jobjectArray pl = plane(e, details, l);
-      if (!pl || !scatter_rows(e, pl, b0, nb, N, pd + (size_t)l * nb * N)) st = VW_ERR_ARG;
-      if (pl) (*e)->DeleteLocalRef(e, pl);
+      if (!scatter_rows(e, pl, b0, nb, N, pd + (size_t)l * nb * N)) st = VW_ERR_ARG;
+      (*e)->DeleteLocalRef(e, pl);
     }
     if (st == VW_OK && !scatter_rows(e, approx, b0, nb, N, pa)) st = VW_ERR_ARG;
   }
@@ -393,9 +423,10 @@ JNIEXPORT jint JNICALL VW_JNI(modwtInverseAoS)(JNIEnv *e, jclass c, jlong ctx, j
   if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n) return VW_ERR_ARG;
   if (!details || !approx || !y) return VW_ERR_NULL;
   const jsize J = (*e)->GetArrayLength(e, details), B = (*e)->GetArrayLength(e, approx), N = row_len(e, approx);
-  if (J < 1) return VW_ERR_ARG;
+  if (J < 1) return arg_error(e, "levels must be > 0");
   if (N < 1) return VW_ERR_EMPTY;
-  if ((*e)->GetArrayLength(e, y) != B) return VW_ERR_ARG;
+  if ((*e)->GetArrayLength(e, y) != B) return arg_error(e, "y must hold one row per signal");
+  if (!planes_ok(e, details, J, B)) return VW_ERR_ARG;
   const jsize CB = chunk_rows((size_t)(J + 2) * (size_t)N, B);
   int oom = 0;
   double *pd = out_buf(0, (size_t)J * CB * N, &oom), *pa = out_buf(1, (size_t)CB * N, &oom);
@@ -406,14 +437,15 @@ JNIEXPORT jint JNICALL VW_JNI(modwtInverseAoS)(JNIEnv *e, jclass c, jlong ctx, j
     const jsize nb = B - b0 < CB ? B - b0 : CB;
     for (jsize l = 0; l < J && st == VW_OK; ++l) {
       jobjectArray pl = plane(e, details, l);
-      if (!pl || (*e)->GetArrayLength(e, pl) != B || !gather_rows(e, pl, b0, nb, N, pd + (size_t)l * nb * N))
-        st = VW_ERR_ARG;
-      if (pl) (*e)->DeleteLocalRef(e, pl);
+      if (!gather_rows(e, pl, b0, nb, N, pd + (size_t)l * nb * N)) st = VW_ERR_ARG;
+      (*e)->DeleteLocalRef(e, pl);
     }
     if (st != VW_OK) break;
     if (!gather_rows(e, approx, b0, nb, N, pa)) { st = VW_ERR_ARG; break; }
+    vw_set_signal_base(b0);
     st = vw_modwt_inverse_f64(CTX(ctx), pd, pa, nb, N, tl.v, th.v, tl.n, wid, boundary, J, 0xFFFFFFFFu, 0,
                               (unsigned)flags | HOST_FLAGS, py);
+    vw_set_signal_base(0);
     if (st == VW_OK && !scatter_rows(e, y, b0, nb, N, py)) st = VW_ERR_ARG;
   }
   trim_slots();
@@ -429,7 +461,7 @@ JNIEXPORT jint JNICALL VW_JNI(swtDenoiseAoS)(JNIEnv *e, jclass c, jlong ctx, job
   if (!x || !y) return VW_ERR_NULL;
   const jsize B = (*e)->GetArrayLength(e, x), N = row_len(e, x);
   if (N < 1) return VW_ERR_EMPTY;
-  if ((*e)->GetArrayLength(e, y) != B) return VW_ERR_ARG;
+  if ((*e)->GetArrayLength(e, y) != B) return arg_error(e, "y must hold one row per signal");
   const jsize CB = chunk_rows(2 * (size_t)N, B);
   int oom = 0;
   double *px = out_buf(0, (size_t)CB * N, &oom), *py = out_buf(1, (size_t)CB * N, &oom);
@@ -438,10 +470,111 @@ JNIEXPORT jint JNICALL VW_JNI(swtDenoiseAoS)(JNIEnv *e, jclass c, jlong ctx, job
   for (jsize b0 = 0; b0 < B && st == VW_OK; b0 += CB) {
     const jsize nb = B - b0 < CB ? B - b0 : CB;
     if (!gather_rows(e, x, b0, nb, N, px)) { st = VW_ERR_ARG; break; }
+    vw_set_signal_base(b0);
     st = vw_swt_denoise_f64(CTX(ctx), px, nb, N, N, tl.v, th.v, tl.n, wid, boundary, J, threshold, soft ? 1 : 0,
                             (unsigned)flags | HOST_FLAGS, py, NULL);
+    vw_set_signal_base(0);
     if (st == VW_OK && !scatter_rows(e, y, b0, nb, N, py)) st = VW_ERR_ARG;
   }
+  trim_slots();
+  return st;
+}
+
+/* ---- VectorWaveSwtAdapter.estimateNoiseSigma (core/swt/VectorWaveSwtAdapter.java:627-645) ---------
+ * sigma[b] = median(|coeffs[b]|) / 0.6745 for B rows of N (flat); exact selection on the device. */
+JNIEXPORT jint JNICALL VW_JNI(noiseSigma)(JNIEnv *e, jclass c, jlong ctx, jdoubleArray coeffs, jint B, jint N,
+                                          jdoubleArray sigmaOut) {
+  (void)c;
+  if (!coeffs || !sigmaOut) return VW_ERR_NULL;
+  const size_t n = (size_t)B * (size_t)N;
+  if (B < 1 || N < 1) return VW_ERR_EMPTY;
+  if (alen(e, coeffs) < n || alen(e, sigmaOut) < (size_t)B) return arg_error(e, "array shorter than B * N");
+  int oom = 0;
+  double *pc = copy_in(e, coeffs, 0, n, &oom), *ps = out_buf(1, (size_t)B, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = vw_noise_sigma_f64(CTX(ctx), pc, B, N, HOST_FLAGS, ps);
+  if (st == VW_OK) copy_out(e, sigmaOut, ps, (size_t)B);
+  trim_slots();
+  return st;
+}
+
+/* ---- BatchStreamingMODWT ZERO_PADDING / SYMMETRIC (ext/extensions/modwt/BatchStreamingMODWT.java:55-380)
+ * over vw_stream_*: the per-level left history lives on the device between blocks.  (PERIODIC blocks are
+ * independent: the Java facade sends them through the BatchMODWT natives, as the reference does.) */
+JNIEXPORT jlong JNICALL VW_JNI(streamCreate)(JNIEnv *e, jclass c, jlong ctx, jdoubleArray lo, jdoubleArray hi,
+                                             jint boundary, jint levels) {
+  (void)c;
+  Taps tl, th;
+  if (!get_taps(e, lo, &tl) || !get_taps(e, hi, &th) || tl.n != th.n) return 0;
+  vw_stream *s = NULL;
+  return vw_stream_create(CTX(ctx), tl.v, th.v, tl.n, boundary, levels, &s) == VW_OK ? (jlong)(intptr_t)s : 0;
+}
+
+JNIEXPORT jint JNICALL VW_JNI(streamDestroy)(JNIEnv *e, jclass c, jlong stream) {
+  (void)e; (void)c;
+  return vw_stream_destroy((vw_stream *)(intptr_t)stream);
+}
+
+JNIEXPORT jlong JNICALL VW_JNI(streamHistoryLength)(JNIEnv *e, jclass c, jlong stream, jint level) {
+  (void)e; (void)c;
+  return vw_stream_history_length((vw_stream *)(intptr_t)stream, level);
+}
+
+/* the stream's level count: the engine writes [levels][B][n] details, so the Java planes must match it */
+static int stream_levels_ok(vw_stream *s, jsize J) {
+  return J >= 1 && vw_stream_history_length(s, J) >= 0 && vw_stream_history_length(s, J + 1) < 0;
+}
+
+/* processSingleLevel / processMultiLevel (:55-175): block [B][n] -> details [levels][B][n], approx [B][n]. */
+JNIEXPORT jint JNICALL VW_JNI(streamProcessAoS)(JNIEnv *e, jclass c, jlong stream, jobjectArray block,
+                                                jobjectArray details, jobjectArray approx) {
+  (void)c;
+  vw_stream *s = (vw_stream *)(intptr_t)stream;
+  if (!s || !block || !details || !approx) return VW_ERR_NULL;
+  const jsize B = (*e)->GetArrayLength(e, block), N = row_len(e, block), J = (*e)->GetArrayLength(e, details);
+  if (B < 1 || N < 1) return arg_error(e, "block must be non-null and non-empty");
+  if (!stream_levels_ok(s, J)) return arg_error(e, "details must hold one plane per configured level");
+  if ((*e)->GetArrayLength(e, approx) != B) return arg_error(e, "approx must hold one row per signal");
+  if (!planes_ok(e, details, J, B)) return VW_ERR_ARG;
+  const size_t n = (size_t)B * (size_t)N;
+  int oom = 0;
+  double *px = out_buf(0, n, &oom), *pd = out_buf(1, (size_t)J * n, &oom), *pa = out_buf(2, n, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  if (!gather_rows(e, block, 0, B, N, px)) { trim_slots(); return VW_ERR_ARG; }
+  vw_status st = vw_stream_process_f64(s, px, B, N, HOST_FLAGS | VW_FLAG_REF_NONFINITE, pd, pa);
+  for (jsize l = 0; l < J && st == VW_OK; ++l) {
+    jobjectArray pl = plane(e, details, l);
+    if (!scatter_rows(e, pl, 0, B, N, pd + (size_t)l * n)) st = VW_ERR_ARG;
+    (*e)->DeleteLocalRef(e, pl);
+  }
+  if (st == VW_OK && !scatter_rows(e, approx, 0, B, N, pa)) st = VW_ERR_ARG;
+  trim_slots();
+  return st;
+}
+
+/* flushSingleLevel / flushMultiLevel (:181-275): the synthetic tail of tailLength samples per signal of the
+ * last block's batch (details [levels][B][tail], approx [B][tail]); the Java side sizes the outputs. */
+JNIEXPORT jint JNICALL VW_JNI(streamFlushAoS)(JNIEnv *e, jclass c, jlong stream, jint tailLength,
+                                              jobjectArray details, jobjectArray approx) {
+  (void)c;
+  vw_stream *s = (vw_stream *)(intptr_t)stream;
+  if (!s || !details || !approx) return VW_ERR_NULL;
+  const jsize B = (*e)->GetArrayLength(e, approx), J = (*e)->GetArrayLength(e, details);
+  if (!stream_levels_ok(s, J)) return arg_error(e, "details must hold one plane per configured level");
+  if (tailLength > 0 && vw_stream_batch(s) > 0 && (int64_t)B != vw_stream_batch(s))
+    return arg_error(e, "flush outputs must hold one row per signal of the last block");
+  if (!planes_ok(e, details, J, B)) return VW_ERR_ARG;
+  const size_t n = (size_t)B * (size_t)(tailLength > 0 ? tailLength : 0);
+  int oom = 0;
+  double *pd = out_buf(1, (size_t)J * n, &oom), *pa = out_buf(2, n, &oom);
+  if (oom) return VW_ERR_DEVICE;
+  vw_status st = vw_stream_flush_f64(s, tailLength, HOST_FLAGS, pd, pa);
+  for (jsize l = 0; l < J && st == VW_OK && tailLength > 0; ++l) {
+    jobjectArray pl = plane(e, details, l);
+    if (!scatter_rows(e, pl, 0, B, tailLength, pd + (size_t)l * n)) st = VW_ERR_ARG;
+    (*e)->DeleteLocalRef(e, pl);
+  }
+  if (st == VW_OK && tailLength > 0 && !scatter_rows(e, approx, 0, B, tailLength, pa)) st = VW_ERR_ARG;
   trim_slots();
   return st;
 }

@@ -1,0 +1,181 @@
+"""Non-finite samples on the reference's unvalidated paths (VW_FLAG_REF_NONFINITE, vectorwave_amd/csrc/vw_ref.hip).
+
+BatchMODWT.multiLevelAoS (no finite check, BatchMODWT.java:201-212) multiplies every tap of the upsampled
+filters, zeros included (BatchSIMDMODWT.java:384-424); so do MultiLevelMODWTTransform.reconstruct (K4-K6,
+:554-645, which BatchMODWT.inverseMultiLevelAoS calls per signal) and VectorWaveSwtAdapter.forwardParallel
+(:210-335; the branch config 3 takes: N >= 4096 and J > 2) / inverse (:435-487).  A NaN or +-Inf sample
+therefore turns every output whose window reaches it through a zero tap into NaN (0 * Inf).  The bar here is
+full identity with the restatement (oracle/vw_oracle.c, which multiplies the zero taps as the reference
+does): NaN masks equal, +-Inf equal, every other value bit-equal (signed zeros included).
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+import vectorwave_amd as vw
+from vectorwave_amd.wavelets import Daubechies, Symlet
+
+pytestmark = pytest.mark.gpu
+
+
+def signals(B, n, seed):
+    return np.stack([O.java_random_signal(n, seed + b) for b in range(B)])
+
+
+def lohi(w):
+    return w.lowPassDecomposition(), w.highPassDecomposition()
+
+
+def same(got, ref, what=""):
+    """Identity: NaN where the reference has NaN, and the same 64 bits everywhere else."""
+    got, ref = np.asarray(got, dtype=np.float64), np.asarray(ref, dtype=np.float64)
+    assert got.shape == ref.shape, what
+    gn, rn = np.isnan(got), np.isnan(ref)
+    if not np.array_equal(gn, rn):
+        bad = np.argwhere(gn != rn)
+        raise AssertionError(f"{what}: NaN masks differ at {len(bad)} positions, first {bad[:4].tolist()}")
+    gb, rb = got[~gn].view(np.int64), ref[~rn].view(np.int64)
+    if not np.array_equal(gb, rb):
+        i = int(np.argmax(gb != rb))
+        raise AssertionError(f"{what}: value {got[~gn][i]!r} != reference {ref[~rn][i]!r}")
+
+
+def poisoned(B, n, seed):
+    """Rows: 0 +Inf, 1 NaN, 2 -Inf next to +Inf (Inf - Inf inside the sums), 3 clean, 4 NaN at both ends."""
+    x = signals(B, n, seed)
+    x[0, n // 5] = np.inf
+    x[1, 7] = np.nan
+    x[2, n // 2] = -np.inf
+    x[2, n // 2 + 1] = np.inf
+    if B > 4:
+        x[4, 0] = np.nan
+        x[4, n - 1] = np.nan
+    return x
+
+
+@pytest.mark.parametrize("case", [(Daubechies.DB4, 512, 4), (Symlet.SYM8, 1024, 5), (Daubechies.DB4, 4096, 6)],
+                         ids=["db4-512-J4", "sym8-1024-J5", "db4-4096-J6"])
+@pytest.mark.parametrize("device", [False, True], ids=["host", "device"])
+def test_batch_modwt_nonfinite_identity(engine, case, device):
+    import torch
+    w, n, J = case
+    x = poisoned(5, n, 51)
+    xin = torch.from_numpy(x).cuda() if device else x
+    m = vw.BatchMODWT.multiLevelAoS(w, xin, J)
+    det = m.detailPerLevel.cpu().numpy() if device else m.detailPerLevel
+    app = m.finalApprox.cpu().numpy() if device else m.finalApprox
+    y = vw.BatchMODWT.inverseMultiLevelAoS(w, m.detailPerLevel, m.finalApprox)
+    y = y.cpu().numpy() if device else y
+    for b in range(5):
+        d_ref, a_ref = O.decompose(x[b], *lohi(w), O.PERIODIC, J, core=False)
+        same(det[:, b, :], d_ref, f"details row {b}")
+        same(app[b], a_ref, f"approx row {b}")
+        if b < 3:
+            assert np.isnan(d_ref).any()  # the zero taps spread the sample as NaN
+        same(y[b], O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC),
+             f"inverse row {b}")
+
+
+def test_batch_modwt_nonfinite_under_fma(engine):
+    # FMA accumulation: the flagged rows run the reference's arithmetic (identical), the clean row stays
+    # within the FMA tolerance
+    w, n, J = Daubechies.DB4, 512, 5
+    x = poisoned(4, n, 77)
+    m = vw.BatchMODWT.multiLevelAoS(w, x, J, fma=True)
+    for b in range(4):
+        d_ref, a_ref = O.decompose(x[b], *lohi(w), O.PERIODIC, J, core=False)
+        if b < 3:
+            same(m.detailPerLevel[:, b, :], d_ref, f"row {b}")
+            same(m.finalApprox[b], a_ref, f"row {b}")
+        else:
+            assert np.max(np.abs(m.detailPerLevel[:, b, :] - d_ref)) <= 1e-12
+            assert np.max(np.abs(m.finalApprox[b] - a_ref)) <= 1e-12
+
+
+def test_batch_modwt_overflow_inside_the_cascade(engine):
+    # finite input whose sums overflow to +-Inf at some level: the next level's zero taps turn it into NaN
+    w, n, J = Daubechies.DB4, 512, 5
+    x = signals(3, n, 5)
+    x[0, 100:140] = 1.7e308
+    x[1, 10:20] = -1.7e308
+    m = vw.BatchMODWT.multiLevelAoS(w, x, J)
+    y = vw.BatchMODWT.inverseMultiLevelAoS(w, m.detailPerLevel, m.finalApprox)
+    for b in range(3):
+        d_ref, a_ref = O.decompose(x[b], *lohi(w), O.PERIODIC, J, core=False)
+        same(m.detailPerLevel[:, b, :], d_ref, f"row {b}")
+        same(m.finalApprox[b], a_ref, f"row {b}")
+        same(y[b], O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(), O.PERIODIC),
+             f"inverse row {b}")
+    assert not np.isfinite(m.finalApprox[0]).all()
+
+
+def test_batch_inverse_of_nonfinite_coefficients(engine):
+    # inverseMultiLevelAoS on coefficients the caller poisoned directly (core reconstruct validates nothing)
+    w, n, J = Symlet.SYM8, 2048, 4
+    x = signals(3, n, 9)
+    m = vw.BatchMODWT.multiLevelAoS(w, x, J)
+    det, app = m.detailPerLevel.copy(), m.finalApprox.copy()
+    det[2, 0, 500] = np.nan
+    app[1, 1000] = -np.inf
+    det[0, 2, 3] = np.inf
+    y = vw.BatchMODWT.inverseMultiLevelAoS(w, det, app)
+    for b in range(3):
+        same(y[b], O.reconstruct(det[:, b, :], app[b], w.lowPassReconstruction(), w.highPassReconstruction(),
+                                 O.PERIODIC), f"row {b}")
+
+
+@pytest.mark.parametrize("soft", [True, False], ids=["soft", "hard"])
+def test_swt_denoise_parallel_branch_nonfinite_config3(engine, soft):
+    # config 3's shape and branch: sym8 J = 8, N = 16384 (forwardParallel: no validation), universal threshold
+    w, n, J = Symlet.SYM8, 16384, 8
+    x = poisoned(4, n, 123)
+    swt = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC)
+    y, thr = swt.denoise(x, J, soft=soft, return_thresholds=True)
+    for b in range(4):
+        y_ref, t_ref = O.swt_denoise(x[b], *lohi(w), O.PERIODIC, J, soft=soft, wavelet_id=w.wavelet_id)
+        same(thr[b], t_ref, f"threshold row {b}")
+        same(y[b], y_ref, f"denoised row {b}")
+
+
+@pytest.mark.parametrize("boundary", [O.PERIODIC, O.SYMMETRIC, O.ZERO_PADDING], ids=["P", "S", "Z"])
+def test_swt_parallel_forward_inverse_nonfinite(engine, boundary):
+    # forwardParallel's three chunk loops (:282-335) and the matching inverse (reconstructPeriodic, or core
+    # reconstruct K5 / K6 with the symmetric alignment)
+    w, n, J = Daubechies.DB4, 4096, 4
+    x = poisoned(5, n, 31)
+    swt = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode(boundary))
+    res = swt.forward(x, J)
+    det, app = res.details_array, res.approximation_array
+    y = swt.inverse(res)
+    for b in range(5):
+        d_ref, a_ref = O.swt_forward(x[b], *lohi(w), boundary, J)
+        same(det[:, b, :], d_ref, f"details row {b}")
+        same(app[b], a_ref, f"approx row {b}")
+        if boundary == O.PERIODIC:
+            y_ref = O.swt_reconstruct_periodic(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction())
+        else:
+            y_ref = O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(), boundary,
+                                  wavelet_id=w.wavelet_id)
+        same(y[b], y_ref, f"inverse row {b}")
+
+
+def test_streaming_periodic_blocks_nonfinite(engine):
+    # BatchStreamingMODWT PERIODIC blocks are independent BatchMODWT blocks (BatchStreamingMODWT.java:110-116)
+    w, n, J = Daubechies.DB4, 1024, 4
+    x = poisoned(3, n, 17)
+    with vw.BatchStreamingMODWT(w, vw.BoundaryMode.PERIODIC, J) as s:
+        r = s.processMultiLevel(x)
+    for b in range(3):
+        d_ref, a_ref = O.decompose(x[b], *lohi(w), O.PERIODIC, J, core=False)
+        same(r.detailPerLevel[:, b, :], d_ref, f"row {b}")
+        same(r.finalApprox[b], a_ref, f"row {b}")
+
+
+def test_validated_paths_still_reject(engine):
+    # the validated entry points keep the reference's InvalidSignalException (VAL_003), first bad index
+    x = signals(1, 512, 3)[0]
+    x[77] = np.nan
+    with pytest.raises(vw.InvalidSignalException):
+        vw.MultiLevelMODWTTransform(Daubechies.DB4, vw.BoundaryMode.PERIODIC).decompose(x, 3)
+    with pytest.raises(vw.InvalidSignalException):  # decomposeSWT branch (N < 4096)
+        vw.VectorWaveSwtAdapter(Daubechies.DB4, vw.BoundaryMode.PERIODIC).forward(x, 3)

@@ -22,6 +22,7 @@ FLAG_HOST_MEMORY = 1 << 4
 FLAG_SYNC = 1 << 5
 FLAG_BATCH_SYM_INVERSE = 1 << 6
 FLAG_BATCH_HAAR = 1 << 7
+FLAG_REF_NONFINITE = 1 << 8
 
 PERIODIC, SYMMETRIC, ZERO_PADDING = 0, 1, 2
 
@@ -40,6 +41,7 @@ SIGNATURES = {
     "vw_last_error": (c_char_p, []),
     "vw_last_error_index": (c_int64, []),
     "vw_version": (c_char_p, []),
+    "vw_set_signal_base": (None, [c_int64]),
     "vw_max_levels": (c_int, [c_int64, c_int]),
     "vw_upsampled_length": (c_int64, [c_int, c_int]),
     "vw_modwt_forward_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_int64, _dp, _dp, c_int, c_int, c_int,
@@ -77,6 +79,7 @@ SIGNATURES = {
     "vw_stream_process_f64": (c_int, [c_void_p, c_void_p, c_int64, c_int64, c_uint, c_void_p, c_void_p]),
     "vw_stream_flush_f64": (c_int, [c_void_p, c_int64, c_uint, c_void_p, c_void_p]),
     "vw_stream_history_length": (c_int64, [c_void_p, c_int]),
+    "vw_stream_batch": (c_int64, [c_void_p]),
     "vw_fill_uniform_f64": (c_int, [c_void_p, c_void_p, c_int64, c_uint64, c_int64]),
     "vw_fill_uniform_f32": (c_int, [c_void_p, c_void_p, c_int64, c_uint64, c_int64]),
     "vw_device_alloc": (c_int, [c_void_p, c_int64, POINTER(c_void_p)]),

@@ -88,7 +88,8 @@ class BatchMODWT:
         x = _validate_aos(signals)
         _check_batch_reach(wavelet, x.shape[1], levels)
         det, app = _engine_for(x).forward(x, wavelet.lowPassDecomposition(), wavelet.highPassDecomposition(),
-                                          wavelet.wavelet_id, nat.PERIODIC, levels, nat.FLAG_FMA if fma else 0)
+                                          wavelet.wavelet_id, nat.PERIODIC, levels,
+                                          nat.FLAG_REF_NONFINITE | (nat.FLAG_FMA if fma else 0))
         return MultiLevelResult(det, app)
 
     @staticmethod
@@ -117,7 +118,7 @@ class BatchMODWT:
         J = det.shape[0]
         return _engine_for(app).inverse(det, app, wavelet.lowPassReconstruction(), wavelet.highPassReconstruction(),
                                         wavelet.wavelet_id, nat.PERIODIC, J,
-                                        nat.FLAG_CORE_LEVELS | (nat.FLAG_FMA if fma else 0))
+                                        nat.FLAG_CORE_LEVELS | nat.FLAG_REF_NONFINITE | (nat.FLAG_FMA if fma else 0))
 
 
 class BatchSIMDMODWT:
@@ -239,7 +240,10 @@ class BatchStreamingMODWT:
         B, n = xa.shape
         det = self._engine._empty(xa, dev, (self.levels, B, n))
         app = self._engine._empty(xa, dev, (B, n))
-        _check(self._engine.lib.vw_stream_process_f64(self._h, xp, B, n, 0 if dev else nat.FLAG_HOST_MEMORY,
+        # PERIODIC blocks are BatchMODWT blocks: the reference's NaN spread through the zero taps
+        # (ZERO / SYMMETRIC blocks with history are not covered by the flag, include/vectorwave_amd.h)
+        fl = (0 if dev else nat.FLAG_HOST_MEMORY) | nat.FLAG_REF_NONFINITE
+        _check(self._engine.lib.vw_stream_process_f64(self._h, xp, B, n, fl,
                                                       self._engine._ptr(det, dev), self._engine._ptr(app, dev)))
         self._B = B  # batch of the last block (sizes the host outputs of a flush)
         return det, app, dev

@@ -827,6 +827,7 @@ extern "C" vw_status vw_ctx_synchronize(vw_ctx* c) {
 extern "C" const char* vw_last_error(void) { return t_err.c_str(); }
 extern "C" int64_t vw_last_error_index(void) { return t_err_index; }
 extern "C" const char* vw_version(void) { return "vectorwave_amd 0.1.0 (gfx950)"; }
+extern "C" void vw_set_signal_base(int64_t base) { t_signal_base = base; }
 
 extern "C" vw_status vw_ctx_enable_timing(vw_ctx* c, int enable) {
   if (!c) return fail(VW_ERR_NULL, "ctx is null");
@@ -1125,6 +1126,45 @@ static void deep_segments(const Tuning& tu, int cus, int64_t B, DeepArgs<T>* a) 
 }
 
 // ------------------------------------------------------------------------------------------------
+// VW_FLAG_REF_NONFINITE (vw_ref.hip): after the fast kernels, flag the rows holding a non-finite value
+// in any of `planes` (the call's inputs and outputs: an overflow to Inf inside the cascade shows in an
+// output), then recompute those rows with the reference's full-tap loops.  Stream-ordered, capturable
+// once the workspace has grown.
+template <typename T>
+static vw_status ref_nonfinite(vw_ctx* c, const std::vector<std::pair<const T*, int64_t>>& planes, RefArgs<T>& r,
+                               bool inverse) {
+  const int64_t B = r.B, N = r.N;
+  if ((int)planes.size() > kRefPlanes) return fail(VW_ERR_ARG, "too many planes for the non-finite scan");
+  const size_t flag_bytes = align_up((size_t)B * sizeof(int), 256);
+  // rows recomputed at once: one workgroup each, two running-approximation rows of scratch (<= 512 MiB)
+  int64_t grid = std::min<int64_t>(B, 2LL * c->cus);
+  grid = std::max<int64_t>(1, std::min<int64_t>(grid, ((int64_t)512 << 20) / (2 * N * (int64_t)sizeof(T))));
+  VW_TRY(ensure_ws(c, flag_bytes + (size_t)grid * 2 * (size_t)N * sizeof(T)));
+  int* flag = reinterpret_cast<int*>(c->ws);
+  VW_HIP(hipMemsetAsync(flag, 0, (size_t)B * sizeof(int), c->stream));
+  RefScan<T> s;
+  memset(&s, 0, sizeof(s));
+  for (const auto& p : planes) {
+    s.p[s.np] = p.first;
+    s.ld[s.np] = p.second;
+    ++s.np;
+  }
+  s.B = B; s.N = (int)N; s.chunks = ref_scan_chunks((int)N); s.flag = flag;
+  LaunchTimer lt(c, "ref_nonfinite");
+  hipError_t e = launch_flag_nonfinite<T>(s, c->stream);
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "non-finite scan launch failed: %s", hipGetErrorString(e));
+  r.flag = flag;
+  r.scratch = reinterpret_cast<T*>(static_cast<char*>(c->ws) + flag_bytes);
+  e = launch_ref_cascade<T>(r, (int)grid, inverse, c->stream);
+  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "reference-arithmetic launch failed: %s", hipGetErrorString(e));
+  return VW_OK;
+}
+
+static int ref_mode(int boundary) {
+  return boundary == VW_PERIODIC ? kHaloPeriodic : boundary == VW_ZERO_PADDING ? kHaloZero : kHaloSymmetric;
+}
+
+// ------------------------------------------------------------------------------------------------
 // Forward (multi-level and single-level share this path).
 template <typename T>
 static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64_t ldx, const double* lo,
@@ -1372,6 +1412,22 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
       src = a.out_a;
       lda = N;
     }
+  }
+  // the unvalidated callers' NaN spread through the zero taps (single level and J = 1 have none)
+  if ((flags & VW_FLAG_REF_NONFINITE) && !validate && !single_level && !hist && J >= 2 &&
+      !(flags & VW_FLAG_FFT_SWITCH)) {
+    const size_t plane = (size_t)B * (size_t)N;
+    std::vector<std::pair<const T*, int64_t>> planes;
+    planes.push_back({x, ldx});
+    for (int j = 0; j < J; ++j) planes.push_back({details + j * plane, N});
+    planes.push_back({approx, N});
+    RefArgs<T> r;
+    memset(&r, 0, sizeof(r));
+    r.x = x; r.ldx = ldx; r.details = details; r.approx = approx;
+    r.B = B; r.N = (int)N; r.J = J; r.L = L; r.mode = ref_mode(boundary);
+    copy_taps(r.lo, lo, L);
+    copy_taps(r.hi, hi, L);
+    VW_TRY(ref_nonfinite<T>(c, planes, r, false));
   }
   if (validate) {
     unsigned long long bad = 0;
@@ -1684,6 +1740,24 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse level launch failed: %s", hipGetErrorString(e));
       cur = a.out_a;
     }
+  }
+  // the unvalidated callers' NaN spread through the zero taps (single level and J = 1 have none)
+  if ((flags & VW_FLAG_REF_NONFINITE) && !single_level && J >= 2) {
+    const size_t plane = (size_t)B * (size_t)N;
+    std::vector<std::pair<const T*, int64_t>> planes;
+    for (int j = 0; j < J; ++j)
+      if (lv[j].use_d) planes.push_back({details + j * plane, N});
+    if (!approx_zero) planes.push_back({approx, N});
+    planes.push_back({y, N});
+    RefArgs<T> r;
+    memset(&r, 0, sizeof(r));
+    r.x = approx_zero ? nullptr : approx; r.det_in = details; r.y = y;
+    r.thr = thr; r.thr_ld = thr_ld; r.soft = soft;
+    r.B = B; r.N = (int)N; r.J = J; r.L = L; r.mode = ref_mode(boundary);
+    copy_taps(r.lo, lo, L);
+    copy_taps(r.hi, hi, L);
+    for (int j = 0; j < J; ++j) r.lv[j] = lv[j];
+    VW_TRY(ref_nonfinite<T>(c, planes, r, true));
   }
   if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
   return VW_OK;
@@ -2483,6 +2557,8 @@ extern "C" vw_status vw_stream_destroy(vw_stream* s) {
   delete s;
   return ok();
 }
+
+extern "C" int64_t vw_stream_batch(vw_stream* s) { return s ? s->last_batch : -1; }
 
 extern "C" int64_t vw_stream_history_length(vw_stream* s, int level) {
   if (!s || level < 1 || level > s->levels) return -1;

@@ -179,6 +179,46 @@ struct DenoiseConsts {
   int n;
 };
 
+// The reference's own arithmetic for rows holding non-finite values (vw_ref.hip, VW_FLAG_REF_NONFINITE).
+constexpr int kRefPlanes = kMaxLevels + 3;
+template <typename T>
+struct RefScan {                // flag[b] = 1 when row b of any plane is non-finite somewhere
+  const T* p[kRefPlanes];
+  long long ld[kRefPlanes];     // row stride of plane k
+  int np;
+  long long B;
+  int N;
+  int chunks;                   // ref_scan_chunks(N)
+  int* flag;                    // [B], zeroed by the caller
+};
+template <typename T>
+struct RefArgs {
+  const T* x;                   // forward: input [B][ldx]; inverse: approximation [B][N] (nullptr = zeros)
+  long long ldx;
+  const T* det_in;              // inverse: details [J][B][N]
+  T* details;                   // forward outputs [J][B][N], [B][N]
+  T* approx;
+  T* y;                         // inverse output [B][N]
+  const T* thr;                 // inverse: thresholds [J][thr_ld] (nullptr = none)
+  long long thr_ld;
+  int soft;
+  long long B;
+  int N;
+  int J;
+  int L;
+  int mode;                     // kHaloPeriodic / kHaloZero / kHaloSymmetric
+  const int* flag;              // rows to recompute
+  T* scratch;                   // [grid][2][N] running approximations
+  T lo[kMaxTaps];               // base taps * 1/sqrt(2), as the fast kernels
+  T hi[kMaxTaps];
+  LevelDesc lv[kMaxLevels];     // inverse: use_d, K6 orientation / offsets
+};
+template <typename T>
+hipError_t launch_flag_nonfinite(const RefScan<T>& a, hipStream_t st);
+template <typename T>
+hipError_t launch_ref_cascade(const RefArgs<T>& a, int grid, bool inverse, hipStream_t st);
+int ref_scan_chunks(int N);
+
 // Raise a kernel's dynamic-LDS limit past the 64 KiB default once per kernel instantiation AND
 // device (the attribute belongs to the device's copy of the function; a call per launch costs host
 // time).  `once` is a static of the caller, unique per kernel instantiation; several host threads

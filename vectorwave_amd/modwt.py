@@ -340,7 +340,8 @@ class MultiLevelMODWTTransform:
         app = None if approx_zero else result.approximation_array
         return _engine_for(result.approximation_array).inverse(
             det, app, w.lowPassReconstruction(), w.highPassReconstruction(), w.wavelet_id, int(self.boundaryMode), J,
-            self._fma | (nat.FLAG_CORE_LEVELS if guard else 0), detail_mask=mask, approx_zero=approx_zero,
+            self._fma | nat.FLAG_REF_NONFINITE | (nat.FLAG_CORE_LEVELS if guard else 0), detail_mask=mask,
+            approx_zero=approx_zero,
             shape=tuple(result.approximation_array.shape))
 
     def reconstruct(self, result: MultiLevelMODWTResult):

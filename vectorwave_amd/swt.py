@@ -62,7 +62,8 @@ class VectorWaveSwtAdapter:
 
     def _forward_flags(self, n: int, levels: int) -> int:
         if self.enableParallel and n >= self.parallelThreshold and levels > 2:
-            return self._fma  # forwardParallel: no validation, no level check
+            # forwardParallel: no validation, no level check, every upsampled tap multiplied (NaN spread)
+            return self._fma | nat.FLAG_REF_NONFINITE
         return nat.FLAG_CORE_LEVELS | nat.FLAG_VALIDATE | self._fma  # decomposeSWT :337-364
 
     def forward(self, signal, levels: Optional[int] = None) -> MutableMultiLevelMODWTResult:
