@@ -10,11 +10,12 @@ import com.morphiqlabs.wavelet.extensions.modwt.BatchMODWT;
  * {@link BatchMODWT.MultiLevelResult}), computed by the engine's HIP kernels -- the north_star hot path
  * (db4 J=6 over 4096 x 4096 is {@code multiLevelAoS} + {@code inverseMultiLevelAoS}).
  *
- * <p>Semantics as the reference: PERIODIC boundary, no level cap on the forward
+ * <p>Semantics as the reference: PERIODIC boundary, no level cap and no finite check on the forward
  * (BatchSIMDMODWT.batchMultiLevelMODWTSoA, :343-424), the inverse = core
  * MultiLevelMODWTTransform.reconstruct per signal (:151-178); the single-level inverse = core
  * MODWTTransform.inverse per signal (:121-139).  Bit-identical to those in EXACT mode (the default,
- * {@link AmdRuntime}).
+ * {@link AmdRuntime}), non-finite samples included: both multi-level calls pass FLAG_REF_NONFINITE, so a
+ * NaN / +-Inf spreads through the zero taps of the upsampled filters exactly as the reference's loops.
  *
  * <p>Memory: {@code double[][]} rows go to the engine without a flattened copy on the Java heap (the native
  * side gathers rows into its staging in chunks of at most 512 MiB), so batches whose B * N or
@@ -62,8 +63,8 @@ public final class AmdBatchMODWT {
         double[][][] details = new double[levels][batch][n];
         double[][] approx = new double[batch][n];
         AmdNative.check(AmdNative.modwtForwardAoS(AmdRuntime.ctx(), signals, wavelet.lowPassDecomposition(),
-                wavelet.highPassDecomposition(), AmdNative.waveletId(wavelet), 0, levels, AmdRuntime.FMA, details,
-                approx));
+                wavelet.highPassDecomposition(), AmdNative.waveletId(wavelet), 0, levels,
+                AmdRuntime.FMA | AmdNative.FLAG_REF_NONFINITE, details, approx));
         return new BatchMODWT.MultiLevelResult(details, approx);
     }
 
@@ -113,7 +114,7 @@ public final class AmdBatchMODWT {
         // core MultiLevelMODWTTransform.reconstruct: its level semantics (FLAG_CORE_LEVELS)
         AmdNative.check(AmdNative.modwtInverseAoS(AmdRuntime.ctx(), detailPerLevel, finalApprox,
                 wavelet.lowPassReconstruction(), wavelet.highPassReconstruction(), AmdNative.waveletId(wavelet), 0,
-                AmdRuntime.FMA | AmdNative.FLAG_CORE_LEVELS, out));
+                AmdRuntime.FMA | AmdNative.FLAG_CORE_LEVELS | AmdNative.FLAG_REF_NONFINITE, out));
         return out;
     }
 

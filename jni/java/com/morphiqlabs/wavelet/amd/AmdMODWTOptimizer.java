@@ -120,6 +120,36 @@ public final class AmdMODWTOptimizer implements MODWTOptimizer {
     }
 
     /**
+     * Equal-length batch inverse, MODWTTransform.inverseBatch's optimized branch (core/modwt/MODWTTransform.java
+     * :531-559, inverseBatchOptimized :619-689: pairwise sums, SYMMETRIC reads t + l -- FLAG_BATCH_SYM_INVERSE).
+     * Not part of the reference's SPI: jni/reference/activate-amd-optimizer.patch adds it as a default method.
+     */
+    public double[][] inverseBatch(double[][] waveletCoeffs, double[][] scalingCoeffs, Wavelet wavelet,
+                                   BoundaryMode boundaryMode) {
+        if (waveletCoeffs == null || scalingCoeffs == null || wavelet == null || boundaryMode == null) {
+            throw new NullPointerException("coefficients, wavelet and boundaryMode must not be null");
+        }
+        final int B = scalingCoeffs.length;
+        if (B == 0 || waveletCoeffs.length != B) return null;
+        final int n = scalingCoeffs[0].length;
+        for (int b = 0; b < B; b++) {
+            if (scalingCoeffs[b].length != n || waveletCoeffs[b].length != n) return null;  // not handled
+        }
+        double[][] out = new double[B][n];
+        final int rows = AmdBatchMODWT.chunkRows(n, B);
+        for (int b0 = 0; b0 < B; b0 += rows) {
+            final int nb = Math.min(rows, B - b0);
+            double[] y = new double[nb * n];
+            AmdNative.check(AmdNative.modwt1Inverse(AmdRuntime.ctx(), AmdBatchMODWT.flatten(scalingCoeffs, b0, nb, n),
+                    AmdBatchMODWT.flatten(waveletCoeffs, b0, nb, n), nb, n, wavelet.lowPassReconstruction(),
+                    wavelet.highPassReconstruction(), AmdNative.boundary(boundaryMode),
+                    AmdNative.FLAG_BATCH_SYM_INVERSE | FMA, y));
+            AmdBatchMODWT.unflatten(y, out, b0, nb, n);
+        }
+        return out;
+    }
+
+    /**
      * Multi-level batch forward, BatchMODWT.multiLevelAoS semantics (ext/extensions/modwt/BatchMODWT.java:90-111:
      * PERIODIC, no level cap).  Not part of the reference's SPI: jni/reference/activate-amd-optimizer.patch adds
      * it to MODWTOptimizer as a default method returning null ("not handled") and makes BatchMODWT.multiLevelAoS

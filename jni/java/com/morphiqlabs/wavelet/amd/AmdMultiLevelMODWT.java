@@ -58,7 +58,10 @@ public final class AmdMultiLevelMODWT {
 
     /**
      * One call for a batch of equal-length signals: element b equals {@code decompose(signals[b], levels)}.
-     * Validation as decompose, per signal, before any work; the error names the first offending signal.
+     * Validation as decompose, per signal; the error names the first offending signal of the batch (the
+     * native side may already have transformed earlier row chunks -- their results are discarded with the
+     * exception).  reconstruct* validate nothing, as the reference's (FLAG_REF_NONFINITE: NaN / +-Inf in a
+     * result spread as the reference's loops spread them).
      */
     public MultiLevelMODWTResult[] decomposeBatch(double[][] signals, int levels) {
         final int n = equalRows(signals);
@@ -135,7 +138,8 @@ public final class AmdMultiLevelMODWT {
         double[] y = new double[n];
         AmdNative.check(AmdNative.modwtInverse(AmdRuntime.ctx(), det, r.getApproximationCoeffs(), 1, n,
                 wavelet.lowPassReconstruction(), wavelet.highPassReconstruction(), AmdNative.waveletId(wavelet),
-                boundary, J, mask, approxZero, AmdNative.FLAG_CORE_LEVELS | AmdRuntime.FMA, y));
+                boundary, J, mask, approxZero,
+                AmdNative.FLAG_CORE_LEVELS | AmdNative.FLAG_REF_NONFINITE | AmdRuntime.FMA, y));
         return y;
     }
 

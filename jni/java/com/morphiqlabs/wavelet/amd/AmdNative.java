@@ -21,7 +21,14 @@ import java.nio.ByteBuffer;
  * <p>One native call per batch.  double[] arguments are copied into native memory and back (no Java
  * array is pinned while the GPU works); the {@code *Direct} methods take direct ByteBuffers and copy
  * nothing.  Every method returns the engine's status; {@link #check(int)} turns it into the exception the
- * reference throws for the same condition (INTEGRATION.md section 3).
+ * reference throws for the same condition (INTEGRATION.md section 3).  Malformed arguments the native glue
+ * finds itself (null or ragged rows, short arrays, bad taps) throw IllegalArgumentException /
+ * NullPointerException from the native call directly.
+ *
+ * <p>Status: the C glue behind these declarations is compiled and exercised against a fake JNIEnv
+ * (tests/test_jni_glue.py); the Java sources of this package have never been compiled here (no JDK in the
+ * build image).  They target Java 21 (pattern matching for instanceof, records) and the reference's jars:
+ * experimental until compiled against them (INTEGRATION.md section 2).
  */
 public final class AmdNative {
     static final boolean LOADED;
@@ -46,6 +53,8 @@ public final class AmdNative {
     public static final int FLAG_FMA = 1 << 3;
     public static final int FLAG_BATCH_SYM_INVERSE = 1 << 6;
     public static final int FLAG_BATCH_HAAR = 1 << 7;
+    /** Unvalidated callers: NaN / +-Inf spread through the zero taps exactly as the reference's loops. */
+    public static final int FLAG_REF_NONFINITE = 1 << 8;
 
     // include/vectorwave_amd.h status codes
     static final int VW_OK = 0, VW_ERR_NULL = 1, VW_ERR_EMPTY = 2, VW_ERR_NONFINITE = 3, VW_ERR_LEVEL = 4,
@@ -92,6 +101,16 @@ public final class AmdNative {
                                       int waveletId, int boundary, int flags, double[][] y);
     static native int swtDenoiseAoS(long ctx, double[][] x, double[] lo, double[] hi, int waveletId, int boundary,
                                     int J, double threshold, boolean soft, int flags, double[][] y);
+
+    // VectorWaveSwtAdapter.estimateNoiseSigma per row of B x N coefficients (exact median on the device)
+    static native int noiseSigma(long ctx, double[] coeffs, int B, int N, double[] sigmaOut);
+
+    // BatchStreamingMODWT ZERO_PADDING / SYMMETRIC: per-level history on the device between blocks
+    static native long streamCreate(long ctx, double[] lo, double[] hi, int boundary, int levels);
+    static native int streamDestroy(long stream);
+    static native long streamHistoryLength(long stream, int level);
+    static native int streamProcessAoS(long stream, double[][] block, double[][][] details, double[][] approx);
+    static native int streamFlushAoS(long stream, int tailLength, double[][][] details, double[][] approx);
 
     // direct (off-heap) buffers, native byte order: no copy, no pinning
     static native int modwtForwardDirect(long ctx, ByteBuffer x, int B, int N, double[] lo, double[] hi,

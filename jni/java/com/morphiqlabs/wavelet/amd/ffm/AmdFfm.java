@@ -32,7 +32,7 @@ import static java.lang.foreign.ValueLayout.JAVA_LONG;
  */
 public final class AmdFfm implements AutoCloseable {
     public static final int FLAG_CORE_LEVELS = 1, FLAG_VALIDATE = 1 << 1, FLAG_FFT_SWITCH = 1 << 2, FLAG_FMA = 1 << 3,
-            FLAG_HOST_MEMORY = 1 << 4, FLAG_SYNC = 1 << 5;
+            FLAG_HOST_MEMORY = 1 << 4, FLAG_SYNC = 1 << 5, FLAG_REF_NONFINITE = 1 << 8;
     public static final int PERIODIC = 0, SYMMETRIC = 1, ZERO_PADDING = 2;
 
     private static final Linker LINKER = Linker.nativeLinker();

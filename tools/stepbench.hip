@@ -111,6 +111,46 @@ int main(int argc, char** argv) {
       fflush(stdout);
     }
   };
+  // the same steps recorded per stream into one HIP graph each (bench.py --launch graph-k), replayed once
+  auto run_graph = [&](int S) {
+    std::vector<hipGraphExec_t> ex(S);
+    for (int p = 0; p < S; ++p) {
+      CHK(hipStreamBeginCapture(st[p], hipStreamCaptureModeThreadLocal));
+      for (int i = 0; i < K; ++i) {
+        const Set& s = sets[i % R];
+        const long long rows = B / S, r0 = p * rows;
+        hipLaunchKernelGGL(fanout<16>, dim3((unsigned)rows), dim3(512), 0, st[p], s.x, s.c, N, plane, J, r0);
+        hipLaunchKernelGGL(fanin, dim3((unsigned)rows), dim3(512), 0, st[p], s.c, s.y, N, plane, J, r0);
+      }
+      hipGraph_t g;
+      CHK(hipStreamEndCapture(st[p], &g));
+      CHK(hipGraphInstantiate(&ex[p], g, nullptr, nullptr, 0));
+      CHK(hipGraphDestroy(g));
+    }
+    for (int w = 0; w < 2; ++w)
+      for (int p = 0; p < S; ++p) CHK(hipGraphLaunch(ex[p], st[p]));
+    CHK(hipDeviceSynchronize());
+    for (int rep = 0; rep < 3; ++rep) {
+      CHK(hipEventRecord(e0, st[0]));
+      for (int p = 1; p < S; ++p) CHK(hipStreamWaitEvent(st[p], e0, 0));
+      for (int p = 0; p < S; ++p) CHK(hipGraphLaunch(ex[p], st[p]));
+      for (int p = 1; p < S; ++p) {
+        CHK(hipEventRecord(done[p], st[p]));
+        CHK(hipStreamWaitEvent(st[0], done[p], 0));
+      }
+      CHK(hipEventRecord(e1, st[0]));
+      CHK(hipEventSynchronize(e1));
+      float ms = 0;
+      CHK(hipEventElapsedTime(&ms, e0, e1));
+      const double per = ms / K;
+      printf("{\"pattern\": \"the step, one graph per stream\", \"streams\": %d, \"rep\": %d, \"ms_per_step\": %.4f, "
+             "\"Msamples_per_s\": %.1f, \"GBps\": %.1f}\n", S, rep, per, plane / (per * 1e-3) / 1e6,
+             step_bytes / (per * 1e-3) / 1e9);
+      fflush(stdout);
+    }
+    for (auto& x : ex) CHK(hipGraphExecDestroy(x));
+  };
+  for (int S : {1, 2, 4, 8}) run_graph(S);
   for (int S : {1, smax}) {
     run("fwd sc1 stores + inv nt (the step)", S, [&](const Set& s, long long rows, long long r0, hipStream_t q) {
       hipLaunchKernelGGL(fanout<16>, dim3((unsigned)rows), dim3(512), 0, q, s.x, s.c, N, plane, J, r0);
