@@ -745,8 +745,13 @@ def run(args, world, rank, local):
     wl = Workload(engines, streams, w, J, rows, N, dtype, pipeline, start, torch, *rot)
     wl.overlap = ov
     footprint = sum(pt.footprint() for pt in wl.parts)
+    # With overlapping launches (K > 1 contexts, overlapped steps) a launch's duration says nothing about the
+    # kernel's own rate: the roofline takes it from a one-context timing after the timed region (below), so the
+    # timed region itself carries no per-kernel event nodes (~4 us each inside a graph; db4 4096 x 4096, same
+    # box: 44.2-44.4K with them, 44.6-44.8K without, profiles/r06/ab_db4_launch_modes.log)
+    events_timed = events and not (K > 1 or overlap)
     (elapsed, host_elapsed), (settle_s, settle_steps), fams, sampled, pass_ms = measure(
-        torch, dist, world, wl, flags, args.launch, args.steps, args.warmup, args.settle, events)
+        torch, dist, world, wl, flags, args.launch, args.steps, args.warmup, args.settle, events_timed)
     elapsed = max_over_ranks(torch, dist, world, elapsed, dev)
     host_elapsed = max_over_ranks(torch, dist, world, host_elapsed, dev)
     value = Bg * N * args.steps / elapsed / 1e6
@@ -931,11 +936,13 @@ def run(args, world, rank, local):
                                 "why": "step i works on set i mod R: no step re-reads an input an earlier step left "
                                        "in the 256 MiB Infinity Cache"},
                 "passes_ms": {f: round(v, 5) for f, v in kpass_ms.items()},
-                "kernel_timing": (f"HIP events around every kernel launch of {sampled} of the {args.steps} timed "
-                                  "steps (event nodes inside the replayed graph)" if args.launch == "graph-k" else
-                                  "HIP events around every launch (engine timer)" if args.launch == "direct"
-                                  else "none") if events else "none",
-                "kernels": kernels,
+                "kernel_timing": ((f"HIP events around every kernel launch of {sampled} of the {args.steps} timed "
+                                   "steps (event nodes inside the replayed graph)" if args.launch == "graph-k" else
+                                   "HIP events around every launch (engine timer)" if args.launch == "direct"
+                                   else "none") if events_timed else
+                                  "none inside the timed region (overlapping launches): the kernels are timed by the "
+                                  "one-context pass of roofline.duration_from" if events else "none"),
+                "kernels": kernels if events_timed else kkernels if roof else {},
                 "other_accumulation": alt,
             },
             "weak_scaling": weak,

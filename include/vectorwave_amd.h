@@ -342,7 +342,9 @@ VW_API vw_status vw_graph_destroy(vw_graph *graph);
  * context, which serialises the steps).  flags: FMA / CORE_LEVELS; SYNC, VALIDATE and HOST_MEMORY are
  * refused (VW_ERR_ARG).  vw_pipeline_run enqueues `steps` steps and returns; vw_pipeline_join makes
  * fwd_ctx's stream wait for every enqueued inverse (then the next run starts with no pending edge).
- * Destroying a context kills its pipelines (run / join then return VW_ERR_STATE). */
+ * Destroying a context kills its pipelines (run / join then return VW_ERR_STATE; a destroy waits for a run
+ * that is issuing its steps); run / join while either context is capturing return VW_ERR_STATE.  As for
+ * every call, a context must not be destroyed while another thread still passes it in. */
 typedef struct vw_pipeline vw_pipeline;
 VW_API vw_status vw_pipeline_create(vw_ctx *fwd_ctx, vw_ctx *inv_ctx, int elem_bytes, int sets, void *const *x,
                                     void *const *details, void *const *approx, void *const *y, int64_t B,

@@ -128,6 +128,12 @@ class Jni:
             assert pend is not None and pend.startswith(expect[0]) and expect[1] in pend, (name, st, pend)
         return st, pend
 
+    def raw(self, name, *args):
+        """A native whose result is not a status (handles, lengths): a fresh call, as a JVM makes it after the
+        previous native's exception was thrown."""
+        self.L.h_clear()
+        return getattr(self.L, PFX + name)(self.env, None, *args)
+
     def last_error(self):
         self.L.h_clear()
         s = getattr(self.L, PFX + "lastError")(self.env, None)
@@ -270,7 +276,7 @@ def test_aos_nonfinite_error_names_the_batch_signal(engine, jni):
     assert st == 3 and pend is None  # VW_ERR_NONFINITE -> AmdNative.check -> InvalidSignalException
     msg = jni.last_error()
     assert "signal 5" in msg and "index 123" in msg, msg
-    assert getattr(jni.L, PFX + "lastErrorIndex")(jni.env, None) == 123
+    assert jni.raw("lastErrorIndex") == 123
 
 
 @pytest.mark.gpu
@@ -376,12 +382,10 @@ def test_stream_natives_match_the_restatement(engine, jni, boundary):
     # BatchStreamingMODWT (ZERO / SYMMETRIC): history kept on the device across blocks, then the flush
     w, J, B, n = Daubechies.DB4, 3, 3, 256
     lo, hi = taps(w)
-    h = getattr(jni.L, PFX + "streamCreate")(jni.env, None, ctx_of(engine), jni.doubles(lo), jni.doubles(hi),
-                                             boundary, J)
+    h = jni.raw("streamCreate", ctx_of(engine), jni.doubles(lo), jni.doubles(hi), boundary, J)
     assert h
     try:
-        assert [getattr(jni.L, PFX + "streamHistoryLength")(jni.env, None, h, j) for j in (1, 2, 3, 4)] == \
-               [7, 14, 28, -1]
+        assert [jni.raw("streamHistoryLength", h, j) for j in (1, 2, 3, 4)] == [7, 14, 28, -1]
         refs = [O.StreamRestatement(lo, hi, boundary, J) for _ in range(B)]
         for blk in range(2):
             x = signals(B, n, 100 + 10 * blk)
@@ -404,4 +408,4 @@ def test_stream_natives_match_the_restatement(engine, jni, boundary):
         jni.call("streamFlushAoS", h, tail, jni.planes(np.zeros((J, 2, tail))), jni.rows(np.zeros((2, tail))),
                  expect=(IAE, "last block"))
     finally:
-        assert getattr(jni.L, PFX + "streamDestroy")(jni.env, None, h) == 0
+        assert jni.raw("streamDestroy", h) == 0

@@ -106,6 +106,8 @@ struct Tuning {
   int sweep2_r = 0;            // VW_SWEEP2_R=32: 32-residue groups even where h allows 64 (0 = widest)
   int sweep2_minb = 64;        // VW_SWEEP2_MINB: blocks a residue class needs for the chained sweeps
   int blk_fwd8 = 1;            // VW_BLK_FWD8=0: fused forward instead of the register-blocked one at NV = 8
+  int mfma = 0;                // VW_MFMA=1|2|3: fp32 FMA PERIODIC forward (1) / inverse (2) / both (3) on the matrix
+                               // cores (vw_mfma.hip)
 };
 
 // One switch of the Tuning struct by its environment name; value < 0 = the default.  Returns false
@@ -149,6 +151,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_SWEEP2_R") t.sweep2_r = v == 32 ? 32 : 0;
   else if (k == "VW_SWEEP2_MINB") t.sweep2_minb = v < 0 ? d.sweep2_minb : v;
   else if (k == "VW_BLK_FWD8") t.blk_fwd8 = v < 0 ? d.blk_fwd8 : v;
+  else if (k == "VW_MFMA") t.mfma = v < 0 ? d.mfma : v;
   else return false;
   return true;
 }
@@ -159,7 +162,7 @@ static const char* const kTuningKeys[] = {
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
     "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8",
-    "VW_DMA_NT", "VW_MULTI_NI"};
+    "VW_DMA_NT", "VW_MULTI_NI", "VW_MFMA"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -657,6 +660,7 @@ struct vw_pipeline {
   hipEvent_t join_ev = nullptr;
   int64_t next = 0;       // index of the next step (selects its buffer set)
   bool dead = false;      // a context was destroyed under it
+  std::mutex mu;          // run / join / kill: a kill waits until an in-flight run has issued its steps
 };
 
 static std::mutex g_pipe_mu;
@@ -677,6 +681,7 @@ static void kill_pipelines_of(vw_ctx* c) {
   std::lock_guard<std::mutex> g(g_pipe_mu);
   for (vw_pipeline* p : g_pipes)
     if (!p->dead && (p->cf == c || p->ci == c)) {
+      std::lock_guard<std::mutex> pg(p->mu);
       hipSetDevice(p->device);
       hipStreamSynchronize(p->cf->stream);
       hipStreamSynchronize(p->ci->stream);
@@ -745,8 +750,12 @@ extern "C" vw_status vw_pipeline_create(vw_ctx* cf, vw_ctx* ci, int elem_bytes, 
 
 extern "C" vw_status vw_pipeline_run(vw_pipeline* p, int64_t steps) {
   if (!p) return fail(VW_ERR_NULL, "pipeline is null");
+  std::lock_guard<std::mutex> pg(p->mu);
   if (p->dead) return fail(VW_ERR_STATE, "a context of this pipeline was destroyed");
   if (steps < 0) return fail(VW_ERR_ARG, "steps must be >= 0");
+  // a capture on either context would record one stream's half of each step and wait on events of the
+  // other, uncaptured stream: an invalid graph
+  if (p->cf->capturing || p->ci->capturing) return fail(VW_ERR_STATE, "a context of this pipeline is capturing");
   hipSetDevice(p->device);
   const bool f32 = p->esz == 4;
   for (int64_t k = 0; k < steps; ++k) {
@@ -778,7 +787,9 @@ extern "C" vw_status vw_pipeline_run(vw_pipeline* p, int64_t steps) {
 
 extern "C" vw_status vw_pipeline_join(vw_pipeline* p) {
   if (!p) return fail(VW_ERR_NULL, "pipeline is null");
+  std::lock_guard<std::mutex> pg(p->mu);
   if (p->dead) return fail(VW_ERR_STATE, "a context of this pipeline was destroyed");
+  if (p->cf->capturing || p->ci->capturing) return fail(VW_ERR_STATE, "a context of this pipeline is capturing");
   hipSetDevice(p->device);
   VW_HIP(hipEventRecord(p->join_ev, p->ci->stream));
   VW_HIP(hipStreamWaitEvent(p->cf->stream, p->join_ev, 0));
@@ -1160,6 +1171,12 @@ static vw_status ref_nonfinite(vw_ctx* c, const std::vector<std::pair<const T*, 
   return VW_OK;
 }
 
+// the matrix-core kernels are fp32 only (vw_mfma.hip); the double overloads are never reached
+static hipError_t mfma_forward(const FwdArgs<float>& a, int lds, hipStream_t st) { return launch_forward_mfma(a, lds, st); }
+static hipError_t mfma_forward(const FwdArgs<double>&, int, hipStream_t) { return hipErrorNotSupported; }
+static hipError_t mfma_inverse(const InvArgs<float>& a, int lds, hipStream_t st) { return launch_inverse_mfma(a, lds, st); }
+static hipError_t mfma_inverse(const InvArgs<double>&, int, hipStream_t) { return hipErrorNotSupported; }
+
 static int ref_mode(int boundary) {
   return boundary == VW_PERIODIC ? kHaloPeriodic : boundary == VW_ZERO_PADDING ? kHaloZero : kHaloSymmetric;
 }
@@ -1294,9 +1311,22 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
         if (blk_lds > kLdsBytes) blk_lds = 0;
       }
     }
+    // fp32 FMA, PERIODIC, long filters: the matrix-core forward (vw_mfma.hip, VW_MFMA bit 0)
+    int mfma_lds = 0;
+    if constexpr (std::is_same<T, float>::value) {
+      bool ok = (tu.mfma & 1) && fma && !single_level && a.vec_io && !validate && !hist && mfma_supported(L, N);
+      for (int j = 0; ok && j < J; ++j) ok = lv[j].mode == kHaloPeriodic;
+      const int H = ok ? mfma_halo(L, J) : 0;
+      if (ok && H <= N && (int64_t)(N + H + 2 * L) * 4 <= kLdsBytes) {
+        a.hlpad = H;
+        a.tap_lds = (int)N + H;
+        mfma_lds = (int)((N + H + 2 * L) * 4);
+      }
+    }
     {
       LaunchTimer lt(c, "forward");
-      hipError_t e = blk_lds ? launch_forward_blk<T>(a, threads, blk_lds, fma, nv, c->stream)
+      hipError_t e = mfma_lds ? mfma_forward(a, mfma_lds, c->stream)
+                   : blk_lds ? launch_forward_blk<T>(a, threads, blk_lds, fma, nv, c->stream)
                    : persist ? launch_forward_persist<T>(a, threads, lds, fma, nv, c->stream)
                              : launch_forward_fused<T>(a, threads, lds, fma, nv, c->stream);
       if (e != hipSuccess) return fail(VW_ERR_DEVICE, "forward launch failed: %s", hipGetErrorString(e));
@@ -1556,8 +1586,20 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     // (A persistent form that loads the next signal's approximation during level 1 was measured
     // slower on MI355X: 3 resident workgroups per CU do not divide the batch evenly, and the dynamic
     // dispatch of one-signal workgroups balances better.)
+    // fp32 FMA, PERIODIC sequential sums, long filters: the matrix-core inverse (vw_mfma.hip, VW_MFMA bit 1)
+    int mfma_lds = 0;
+    if constexpr (std::is_same<T, float>::value) {
+      bool ok = (tu.mfma & 2) && fma && !pair && boundary == VW_PERIODIC && a.vec_io && mfma_supported(L, N);
+      for (int j = 0; ok && j < J; ++j) ok = lv[j].dir_a == 1 && lv[j].dir_d == 1 && lv[j].off_a == 0 && lv[j].off_d == 0;
+      const int H = ok ? mfma_halo(L, J) : 0;
+      if (ok && H <= N && (int64_t)(N + H + 2 * L) * 4 <= kLdsBytes) {
+        a.hlpad_a = H;
+        a.tap_lds = (int)N + H;
+        mfma_lds = (int)((N + H + 2 * L) * 4);
+      }
+    }
     LaunchTimer lt(c, "inverse");
-    hipError_t e = launch_inverse_fused<T>(a, threads, lds, fma, nv, c->stream);
+    hipError_t e = mfma_lds ? mfma_inverse(a, mfma_lds, c->stream) : launch_inverse_fused<T>(a, threads, lds, fma, nv, c->stream);
     if (e != hipSuccess) return fail(VW_ERR_DEVICE, "inverse launch failed: %s", hipGetErrorString(e));
   } else {
     // 1024-sample tiles: two LDS regions of ~9 KiB keep many workgroups per CU (measured best on

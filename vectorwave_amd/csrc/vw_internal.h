@@ -219,6 +219,12 @@ template <typename T>
 hipError_t launch_ref_cascade(const RefArgs<T>& a, int grid, bool inverse, hipStream_t st);
 int ref_scan_chunks(int N);
 
+// Matrix-core fp32 kernels (vw_mfma.hip): which (L, N) are instantiated, the halo a level set needs, launchers.
+bool mfma_supported(int L, long long N);
+int mfma_halo(int L, int J);
+hipError_t launch_forward_mfma(const FwdArgs<float>& a, int lds, hipStream_t st);
+hipError_t launch_inverse_mfma(const InvArgs<float>& a, int lds, hipStream_t st);
+
 // Raise a kernel's dynamic-LDS limit past the 64 KiB default once per kernel instantiation AND
 // device (the attribute belongs to the device's copy of the function; a call per launch costs host
 // time).  `once` is a static of the caller, unique per kernel instantiation; several host threads
