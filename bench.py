@@ -101,6 +101,10 @@ def parse(argv=None):
     p.add_argument("--exact", action="store_true",
                    help="headline in EXACT accumulation (bit-identical to vectorwave-core) instead of FMA")
     p.add_argument("--no-alt", action="store_true", help="skip the timing of the other accumulation mode")
+    p.add_argument("--ref-nonfinite", default="off", choices=["on", "off"],
+                   help="VW_FLAG_REF_NONFINITE (the unvalidated batch facade's NaN/Inf spread, vw_ref.hip) on the "
+                        "timed calls: identical results for finite data; db4's kernels probe their rows in-line "
+                        "and each pass adds one fix-up launch (-2.5 %%, profiles/r06/ab_db4_ref_nonfinite_on_off.log)")
     p.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling measurement")
     p.add_argument("--launch", default="graph-k", choices=sorted(LAUNCH_DESC),
                    help="how the timed steps are issued (see measure())")
@@ -735,6 +739,9 @@ def run(args, world, rank, local):
     main = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(main)
     flags = 0 if args.exact else nat.FLAG_FMA
+    ref_nf = args.ref_nonfinite == "on"
+    if ref_nf:
+        flags |= nat.FLAG_REF_NONFINITE
     events = args.events == "inline"
 
     # ---- strong scaling (headline): rank r owns rows [start, start + rows) of the global batch
@@ -923,6 +930,9 @@ def run(args, world, rank, local):
                 "workload": f"{wname} MODWT J={J} {pipeline}, global batch {Bg} x {N} samples, {dtype}, PERIODIC",
                 "wavelet": wname, "levels": J, "global_batch": Bg, "batch_per_gpu": rows, "signal_length": N,
                 "boundary": "PERIODIC", "accumulation": acc_name(args.config, bool(flags & nat.FLAG_FMA)),
+                "nonfinite": ("VW_FLAG_REF_NONFINITE: the batch facade's NaN/Inf spread reproduced (rows probed "
+                              "in-line by the kernels, a fix-up launch per pass)" if ref_nf else
+                              "not emulated in the timed calls (VW_FLAG_REF_NONFINITE off)"),
                 "parallelism": f"batch-shard x{world} (contiguous row blocks, no collective)"
                                + (f", {K} contexts per GPU (own stream each, row blocks)" if K > 1 else "")
                                + (", consecutive steps pipelined over two contexts (step i+1's forward beside "

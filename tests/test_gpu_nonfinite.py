@@ -179,3 +179,60 @@ def test_validated_paths_still_reject(engine):
         vw.MultiLevelMODWTTransform(Daubechies.DB4, vw.BoundaryMode.PERIODIC).decompose(x, 3)
     with pytest.raises(vw.InvalidSignalException):  # decomposeSWT branch (N < 4096)
         vw.VectorWaveSwtAdapter(Daubechies.DB4, vw.BoundaryMode.PERIODIC).forward(x, 3)
+
+
+def test_headline_kernels_flag_their_own_rows(engine):
+    # db4 J = 6, N = 4096, fp64 FMA at 640 rows (> 2 per CU): the persistent forward and the one-buffer
+    # sequential inverse -- the headline's kernels -- probe their own outputs / inputs (no scan pass,
+    # timing family "ref_nonfinite", not "ref_nonfinite_scan").  Poisoned rows: the reference's bits;
+    # clean rows: the fast kernels' bits (the same as without the flag); the flags are clear afterwards.
+    import torch
+    from vectorwave_amd import _native as nat
+    w, n, J, B = Daubechies.DB4, 4096, 6, 640
+    x = O.fill_uniform(B * n, 23).reshape(B, n)
+    x[0, 9] = np.inf
+    x[317, 2048] = np.nan
+    x[B - 1, n - 1] = -np.inf
+    x[B - 1, 0] = np.inf
+    lo, hi = lohi(w)
+    lr, hr = w.lowPassReconstruction(), w.highPassReconstruction()
+    F, REF = nat.FLAG_FMA, nat.FLAG_FMA | nat.FLAG_REF_NONFINITE
+    xt = torch.from_numpy(x).cuda()
+    engine.enable_timing(True)
+    engine.reset_timing()
+    try:
+        d1, a1 = engine.forward(xt, lo, hi, w.wavelet_id, O.PERIODIC, J, REF)
+        det = d1.clone()
+        app = a1.clone()
+        det[2, 100, 7] = float("nan")  # poisoned coefficients of clean rows 100 and 200
+        app[200, 5] = float("inf")
+        y1 = engine.inverse(det, app, lr, hr, w.wavelet_id, O.PERIODIC, J, REF)
+        torch.cuda.synchronize()
+        assert engine.kernel_time("ref_nonfinite")[1] == 2
+        assert engine.kernel_time("ref_nonfinite_scan")[1] == 0
+    finally:
+        engine.enable_timing(False)
+    d0, a0 = engine.forward(xt, lo, hi, w.wavelet_id, O.PERIODIC, J, F)
+    y0 = engine.inverse(det, app, lr, hr, w.wavelet_id, O.PERIODIC, J, F)
+    d1, a1, y1 = d1.cpu().numpy(), a1.cpu().numpy(), y1.cpu().numpy()
+    d0, a0, y0 = d0.cpu().numpy(), a0.cpu().numpy(), y0.cpu().numpy()
+    dh, ah = det.cpu().numpy(), app.cpu().numpy()
+    for b in (0, 317, B - 1):
+        d_ref, a_ref = O.decompose(x[b], lo, hi, O.PERIODIC, J, core=False)
+        same(d1[:, b, :], d_ref, f"details row {b}")
+        same(a1[b], a_ref, f"approx row {b}")
+    for b in (0, 100, 200, 317, B - 1):
+        same(y1[b], O.reconstruct(dh[:, b, :], ah[b], lr, hr, O.PERIODIC), f"inverse row {b}")
+    clean = np.setdiff1d(np.arange(B), [0, 317, B - 1])
+    assert np.array_equal(d1[:, clean, :].view(np.int64), d0[:, clean, :].view(np.int64))
+    assert np.array_equal(a1[clean].view(np.int64), a0[clean].view(np.int64))
+    clean_y = np.setdiff1d(clean, [100, 200])
+    assert np.array_equal(y1[clean_y].view(np.int64), y0[clean_y].view(np.int64))
+    # flags cleared: a clean call with the flag gives the fast kernels' bits everywhere
+    xc = torch.from_numpy(np.nan_to_num(x, nan=0.0, posinf=0.0, neginf=0.0)).cuda()
+    d2, a2 = engine.forward(xc, lo, hi, w.wavelet_id, O.PERIODIC, J, REF)
+    d3, a3 = engine.forward(xc, lo, hi, w.wavelet_id, O.PERIODIC, J, F)
+    y2 = engine.inverse(d2, a2, lr, hr, w.wavelet_id, O.PERIODIC, J, REF)
+    y3 = engine.inverse(d3, a3, lr, hr, w.wavelet_id, O.PERIODIC, J, F)
+    assert torch.equal(d2.view(torch.int64), d3.view(torch.int64)) and torch.equal(a2.view(torch.int64), a3.view(torch.int64))
+    assert torch.equal(y2.view(torch.int64), y3.view(torch.int64))

@@ -8,6 +8,10 @@
 #   pmc:<cfg>:<args>             FETCH_SIZE / WRITE_SIZE passes -> gpurun_out/hbm_traffic_<cfg>.json
 #                                (one context: pass --contexts 1; VW_COMMIT=<sha> stamps captured_at)
 #   grp:<args>                   prof:<args>, then the trace grouped per launch shape -> gpurun_out/prof_<n>_groups.txt
+#   smoke:                       __graft_entry__.smoke() -> gpurun_out/smoke.log
+#   cfg:<config>                 bench.py --config <config> (10 steps, no CPU leg) -> gpurun_out/bench_<config>.json
+#   rehearse:<ranks>             the multi-rank launcher with <ranks> ranks on this one GPU (VW_BENCH_DEVICE_MOD=1)
+#                                -> gpurun_out/bench_db4_<ranks>rank_rehearsal.json
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 mkdir -p gpurun_out
 export TMPDIR=/tmp
@@ -55,6 +59,22 @@ WRITE_SIZE" BENCH_ARGS="--config $cfg $bargs" bash tools/pmc.sh; rc=$?
         cat "gpurun_out/hbm_traffic_$cfg.json"
       fi
       echo "[$s] rc=$rc"; fatal $rc && exit $rc ;;
+    smoke)
+      timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; rc=$?
+      tail -2 gpurun_out/smoke.log; echo "[$s] rc=$rc"
+      [ $rc -ne 0 ] && exit $rc ;;
+    cfg)
+      timeout -k 10 300 python bench.py --config "$arg" --no-cpu-baseline --steps 10 --warmup 3 \
+        > "gpurun_out/bench_$arg.json" 2> "gpurun_out/bench_$arg.err"; rc=$?
+      tail -c 300 "gpurun_out/bench_$arg.json"; echo; echo "[$s] rc=$rc"
+      [ $rc -ne 0 ] && { tail -5 "gpurun_out/bench_$arg.err"; exit $rc; } ;;
+    rehearse)
+      VW_BENCH_DEVICE_MOD=1 timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$arg" \
+        --master-addr 127.0.0.1 --master-port $((29500 + arg)) bench.py --gpus "$arg" --steps 20 --warmup 3 \
+        --no-cpu-baseline --no-alt > "gpurun_out/bench_db4_${arg}rank_rehearsal.json" \
+        2> "gpurun_out/bench_db4_${arg}rank_rehearsal.err"; rc=$?
+      tail -c 300 "gpurun_out/bench_db4_${arg}rank_rehearsal.json"; echo; echo "[$s] rc=$rc"
+      [ $rc -ne 0 ] && exit $rc ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done

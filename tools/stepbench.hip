@@ -26,6 +26,8 @@ template <int AUX>
 __global__ void __launch_bounds__(512) fanout(const double* __restrict__ x, double* __restrict__ out, int N,
                                               long long plane, int J, long long row0) {
   const long long b = row0 + blockIdx.x;
+  extern __shared__ double lds_hold[];  // the LDS footprint of the product kernels (argv[2]), never used
+  if (N < 0) lds_hold[threadIdx.x] = 0;
   const int nv = N / 2;
   d2 v[4];
 #pragma unroll
@@ -47,6 +49,8 @@ __global__ void __launch_bounds__(512) fanout(const double* __restrict__ x, doub
 __global__ void __launch_bounds__(512) fanin(const double* __restrict__ in, double* __restrict__ y, int N,
                                              long long plane, int J, long long row0) {
   const long long b = row0 + blockIdx.x;
+  extern __shared__ double lds_hold[];
+  if (N < 0) lds_hold[threadIdx.x] = 0;
   d2 acc[4] = {};
   for (int j = 0; j < J; ++j) {
 #pragma unroll
@@ -71,6 +75,12 @@ int main(int argc, char** argv) {
   }
   const double step_bytes = plane * 8.0 * 16;  // 1 + 7 planes forward, 7 + 1 inverse
   int smax = argc > 1 ? atoi(argv[1]) : 4;
+  // ./stepbench S LDS_FWD LDS_INV: graph mode only, each workgroup holding that much LDS (bytes) -- the
+  // product kernels' footprint (persistent forward: two level buffers; inverse: one), so that the streams'
+  // passes can share a CU only as far as the product's can
+  const int lds_f = argc > 2 ? atoi(argv[2]) : 0, lds_i = argc > 3 ? atoi(argv[3]) : 0;
+  CHK(hipFuncSetAttribute((const void*)fanout<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+  CHK(hipFuncSetAttribute((const void*)fanin, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
   std::vector<hipStream_t> st(8);
   for (auto& s : st) CHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   hipEvent_t e0, e1;
@@ -119,8 +129,8 @@ int main(int argc, char** argv) {
       for (int i = 0; i < K; ++i) {
         const Set& s = sets[i % R];
         const long long rows = B / S, r0 = p * rows;
-        hipLaunchKernelGGL(fanout<16>, dim3((unsigned)rows), dim3(512), 0, st[p], s.x, s.c, N, plane, J, r0);
-        hipLaunchKernelGGL(fanin, dim3((unsigned)rows), dim3(512), 0, st[p], s.c, s.y, N, plane, J, r0);
+        hipLaunchKernelGGL(fanout<16>, dim3((unsigned)rows), dim3(512), lds_f, st[p], s.x, s.c, N, plane, J, r0);
+        hipLaunchKernelGGL(fanin, dim3((unsigned)rows), dim3(512), lds_i, st[p], s.c, s.y, N, plane, J, r0);
       }
       hipGraph_t g;
       CHK(hipStreamEndCapture(st[p], &g));
@@ -143,14 +153,15 @@ int main(int argc, char** argv) {
       float ms = 0;
       CHK(hipEventElapsedTime(&ms, e0, e1));
       const double per = ms / K;
-      printf("{\"pattern\": \"the step, one graph per stream\", \"streams\": %d, \"rep\": %d, \"ms_per_step\": %.4f, "
-             "\"Msamples_per_s\": %.1f, \"GBps\": %.1f}\n", S, rep, per, plane / (per * 1e-3) / 1e6,
-             step_bytes / (per * 1e-3) / 1e9);
+      printf("{\"pattern\": \"the step, one graph per stream\", \"lds_fwd\": %d, \"lds_inv\": %d, \"streams\": %d, "
+             "\"rep\": %d, \"ms_per_step\": %.4f, \"Msamples_per_s\": %.1f, \"GBps\": %.1f}\n", lds_f, lds_i, S, rep, per,
+             plane / (per * 1e-3) / 1e6, step_bytes / (per * 1e-3) / 1e9);
       fflush(stdout);
     }
     for (auto& x : ex) CHK(hipGraphExecDestroy(x));
   };
   for (int S : {1, 2, 4, 8}) run_graph(S);
+  if (argc > 2) return 0;
   for (int S : {1, smax}) {
     run("fwd sc1 stores + inv nt (the step)", S, [&](const Set& s, long long rows, long long r0, hipStream_t q) {
       hipLaunchKernelGGL(fanout<16>, dim3((unsigned)rows), dim3(512), 0, q, s.x, s.c, N, plane, J, r0);

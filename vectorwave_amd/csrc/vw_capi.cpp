@@ -106,6 +106,7 @@ struct Tuning {
   int sweep2_r = 0;            // VW_SWEEP2_R=32: 32-residue groups even where h allows 64 (0 = widest)
   int sweep2_minb = 64;        // VW_SWEEP2_MINB: blocks a residue class needs for the chained sweeps
   int blk_fwd8 = 1;            // VW_BLK_FWD8=0: fused forward instead of the register-blocked one at NV = 8
+  int ref_grid = 0;            // VW_REF_GRID: workgroups of the REF_NONFINITE fix-up launch (0 = 2 per CU)
   int mfma = 0;                // VW_MFMA=1|2|3: fp32 FMA PERIODIC forward (1) / inverse (2) / both (3) on the matrix
                                // cores (vw_mfma.hip)
 };
@@ -152,6 +153,7 @@ static bool set_tuning(Tuning& t, const char* key, int v) {
   else if (k == "VW_SWEEP2_MINB") t.sweep2_minb = v < 0 ? d.sweep2_minb : v;
   else if (k == "VW_BLK_FWD8") t.blk_fwd8 = v < 0 ? d.blk_fwd8 : v;
   else if (k == "VW_MFMA") t.mfma = v < 0 ? d.mfma : v;
+  else if (k == "VW_REF_GRID") t.ref_grid = v < 0 ? d.ref_grid : v;
   else return false;
   return true;
 }
@@ -162,7 +164,7 @@ static const char* const kTuningKeys[] = {
     "VW_UNROLL_MAX", "VW_BLK", "VW_FWD_NV",
     "VW_INV_NV", "VW_DEEP", "VW_DEEP_INV", "VW_DEEP_LDS", "VW_DEEP_WAVES", "VW_DEEP_PF_FWD", "VW_DEEP_PF_INV",
     "VW_SWEEP2", "VW_SWEEP2_KA", "VW_SWEEP2_UC", "VW_SWEEP2_R", "VW_SWEEP2_MINB", "VW_BLK_FWD8",
-    "VW_DMA_NT", "VW_MULTI_NI", "VW_MFMA"};
+    "VW_DMA_NT", "VW_MULTI_NI", "VW_MFMA", "VW_REF_GRID"};
 
 static Tuning read_tuning() {
   Tuning t;
@@ -203,6 +205,8 @@ struct vw_ctx {
   std::vector<std::pair<void*, size_t>> stage;  // host-memory staging pool (Staging), kept across calls
   void* med = nullptr;         // vw_median_f64 deviations of long rows (not ws: growing ws invalidates graphs)
   size_t med_bytes = 0;
+  int* nf = nullptr;           // VW_FLAG_REF_NONFINITE row flags [nf_rows], zero between calls (vw_ref.hip)
+  int64_t nf_rows = 0;
 };
 
 struct vw_graph {
@@ -342,6 +346,25 @@ static vw_status ensure_ws(vw_ctx* c, size_t bytes) {
   size_t want = std::max(bytes, (size_t)1 << 20);
   VW_HIP(hipMalloc(&c->ws, want));
   c->ws_bytes = want;
+  return VW_OK;
+}
+
+// the REF_NONFINITE row flags: zeroed once at allocation, kept zero by the kernels that consume them
+static vw_status ensure_nf(vw_ctx* c, int64_t B) {
+  if (B <= c->nf_rows) return VW_OK;
+  if (c->capturing) return fail(VW_ERR_STATE, "row-flag growth during capture: run the call once before capturing it");
+  if (c->nf) {
+    hipDeviceSynchronize();
+    ++c->ws_gen;
+    hipFree(c->nf);
+    c->nf = nullptr;
+    c->nf_rows = 0;
+  }
+  const int64_t rows = std::max<int64_t>(B, 4096);
+  VW_HIP(hipMalloc(&c->nf, (size_t)rows * sizeof(int)));
+  VW_HIP(hipMemset(c->nf, 0, (size_t)rows * sizeof(int)));
+  VW_HIP(hipDeviceSynchronize());
+  c->nf_rows = rows;
   return VW_OK;
 }
 
@@ -489,6 +512,7 @@ extern "C" vw_status vw_ctx_destroy(vw_ctx* c) {
   if (c->ws) hipFree(c->ws);
   if (c->ws2) hipFree(c->ws2);
   if (c->med) hipFree(c->med);
+  if (c->nf) hipFree(c->nf);
   for (auto& b : c->stage) hipFree(b.first);
   if (c->bad) hipFree(c->bad);
   if (c->own_stream) hipStreamDestroy(c->stream);
@@ -1143,29 +1167,32 @@ static void deep_segments(const Tuning& tu, int cus, int64_t B, DeepArgs<T>* a) 
 // once the workspace has grown.
 template <typename T>
 static vw_status ref_nonfinite(vw_ctx* c, const std::vector<std::pair<const T*, int64_t>>& planes, RefArgs<T>& r,
-                               bool inverse) {
+                               bool inverse, bool flagged) {
   const int64_t B = r.B, N = r.N;
   if ((int)planes.size() > kRefPlanes) return fail(VW_ERR_ARG, "too many planes for the non-finite scan");
-  const size_t flag_bytes = align_up((size_t)B * sizeof(int), 256);
   // rows recomputed at once: one workgroup each, two running-approximation rows of scratch (<= 512 MiB)
-  int64_t grid = std::min<int64_t>(B, 2LL * c->cus);
+  int64_t grid = std::min<int64_t>(B, c->tune.ref_grid > 0 ? c->tune.ref_grid : 2LL * c->cus);
   grid = std::max<int64_t>(1, std::min<int64_t>(grid, ((int64_t)512 << 20) / (2 * N * (int64_t)sizeof(T))));
-  VW_TRY(ensure_ws(c, flag_bytes + (size_t)grid * 2 * (size_t)N * sizeof(T)));
-  int* flag = reinterpret_cast<int*>(c->ws);
-  VW_HIP(hipMemsetAsync(flag, 0, (size_t)B * sizeof(int), c->stream));
-  RefScan<T> s;
-  memset(&s, 0, sizeof(s));
-  for (const auto& p : planes) {
-    s.p[s.np] = p.first;
-    s.ld[s.np] = p.second;
-    ++s.np;
+  VW_TRY(ensure_nf(c, B));
+  VW_TRY(ensure_ws(c, (size_t)grid * 2 * (size_t)N * sizeof(T)));
+  // timing families: "ref_nonfinite" (the cascade over rows the fast kernel flagged), "ref_nonfinite_scan"
+  // (scan + cascade)
+  LaunchTimer lt(c, flagged ? "ref_nonfinite" : "ref_nonfinite_scan");
+  hipError_t e;
+  if (!flagged) {  // the fast kernel did not probe its rows: scan the call's planes
+    RefScan<T> s;
+    memset(&s, 0, sizeof(s));
+    for (const auto& p : planes) {
+      s.p[s.np] = p.first;
+      s.ld[s.np] = p.second;
+      ++s.np;
+    }
+    s.B = B; s.N = (int)N; s.chunks = ref_scan_chunks((int)N); s.flag = c->nf;
+    e = launch_flag_nonfinite<T>(s, c->stream);
+    if (e != hipSuccess) return fail(VW_ERR_DEVICE, "non-finite scan launch failed: %s", hipGetErrorString(e));
   }
-  s.B = B; s.N = (int)N; s.chunks = ref_scan_chunks((int)N); s.flag = flag;
-  LaunchTimer lt(c, "ref_nonfinite");
-  hipError_t e = launch_flag_nonfinite<T>(s, c->stream);
-  if (e != hipSuccess) return fail(VW_ERR_DEVICE, "non-finite scan launch failed: %s", hipGetErrorString(e));
-  r.flag = flag;
-  r.scratch = reinterpret_cast<T*>(static_cast<char*>(c->ws) + flag_bytes);
+  r.flag = c->nf;
+  r.scratch = reinterpret_cast<T*>(c->ws);
   e = launch_ref_cascade<T>(r, (int)grid, inverse, c->stream);
   if (e != hipSuccess) return fail(VW_ERR_DEVICE, "reference-arithmetic launch failed: %s", hipGetErrorString(e));
   return VW_OK;
@@ -1230,6 +1257,10 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
   // or streaming history.  VW_FWD_PERSIST=0 disables it.
   const Tuning& tu = c->tune;
   const bool persist_on = tu.fwd_persist;
+  // the unvalidated callers' NaN spread through the zero taps (single level and J = 1 have none)
+  const bool ref_nf = (flags & VW_FLAG_REF_NONFINITE) && !validate && !single_level && !hist && J >= 2 &&
+                      !(flags & VW_FLAG_FFT_SWITCH);
+  bool nf_probed = false;
   const bool io_aligned = (ldx % V == 0) && (N % V == 0) && aligned16(x) && aligned16(details) && aligned16(approx);
   auto persist_ok = [&](int th, int nvv, bool ft) {
     return persist_on && io_aligned && ft && nvv == 4 && !validate && !hist && (int64_t)th * nvv == nvec &&
@@ -1322,6 +1353,12 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
         a.tap_lds = (int)N + H;
         mfma_lds = (int)((N + H + 2 * L) * 4);
       }
+    }
+    // VW_FLAG_REF_NONFINITE: the persistent forward probes its own outputs (no scan pass afterwards)
+    if (ref_nf && persist && !mfma_lds && !blk_lds) {
+      VW_TRY(ensure_nf(c, B));
+      a.nf_flag = c->nf;
+      nf_probed = true;
     }
     {
       LaunchTimer lt(c, "forward");
@@ -1443,9 +1480,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
       lda = N;
     }
   }
-  // the unvalidated callers' NaN spread through the zero taps (single level and J = 1 have none)
-  if ((flags & VW_FLAG_REF_NONFINITE) && !validate && !single_level && !hist && J >= 2 &&
-      !(flags & VW_FLAG_FFT_SWITCH)) {
+  if (ref_nf) {
     const size_t plane = (size_t)B * (size_t)N;
     std::vector<std::pair<const T*, int64_t>> planes;
     planes.push_back({x, ldx});
@@ -1457,7 +1492,7 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     r.B = B; r.N = (int)N; r.J = J; r.L = L; r.mode = ref_mode(boundary);
     copy_taps(r.lo, lo, L);
     copy_taps(r.hi, hi, L);
-    VW_TRY(ref_nonfinite<T>(c, planes, r, false));
+    VW_TRY(ref_nonfinite<T>(c, planes, r, false, nf_probed));
   }
   if (validate) {
     unsigned long long bad = 0;
@@ -1483,6 +1518,9 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   const int64_t nvec = (N + V - 1) / V;
   const int tmax = (int)(nvec * V - 1);
   const bool pair = single_level || boundary == VW_ZERO_PADDING;
+  // the unvalidated callers' NaN spread through the zero taps (single level and J = 1 have none)
+  const bool ref_nf = (flags & VW_FLAG_REF_NONFINITE) && !single_level && J >= 2;
+  bool nf_probed = false;
 
   std::vector<LevelDesc> lv(J);
   int max_hl = 0, max_hr = 0;
@@ -1597,6 +1635,14 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         a.tap_lds = (int)N + H;
         mfma_lds = (int)((N + H + 2 * L) * 4);
       }
+    }
+    // VW_FLAG_REF_NONFINITE: the one-buffer sequential kernel (vw_inv.hip's choice) probes its inputs and
+    // output itself (no scan pass afterwards)
+    const bool inv_blk = a.blk && a.unrolled && has_unrolled_taps(L) && nv != 2;
+    if (ref_nf && !mfma_lds && !a.pair && !a.db && !inv_blk) {
+      VW_TRY(ensure_nf(c, B));
+      a.nf_flag = c->nf;
+      nf_probed = true;
     }
     LaunchTimer lt(c, "inverse");
     hipError_t e = mfma_lds ? mfma_inverse(a, mfma_lds, c->stream) : launch_inverse_fused<T>(a, threads, lds, fma, nv, c->stream);
@@ -1783,8 +1829,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       cur = a.out_a;
     }
   }
-  // the unvalidated callers' NaN spread through the zero taps (single level and J = 1 have none)
-  if ((flags & VW_FLAG_REF_NONFINITE) && !single_level && J >= 2) {
+  if (ref_nf) {
     const size_t plane = (size_t)B * (size_t)N;
     std::vector<std::pair<const T*, int64_t>> planes;
     for (int j = 0; j < J; ++j)
@@ -1799,7 +1844,7 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     copy_taps(r.lo, lo, L);
     copy_taps(r.hi, hi, L);
     for (int j = 0; j < J; ++j) r.lv[j] = lv[j];
-    VW_TRY(ref_nonfinite<T>(c, planes, r, true));
+    VW_TRY(ref_nonfinite<T>(c, planes, r, true, nf_probed));
   }
   if (flags & VW_FLAG_SYNC) VW_HIP(hipStreamSynchronize(c->stream));
   return VW_OK;

@@ -728,9 +728,32 @@ __device__ __forceinline__ void zero_regs(T (&r)[NV][VT<T>::V]) {
 // Level inputs alternate between two LDS buffers (p.region1 != 0): level j reads X while its
 // approximation -- the input of level j+1, halo included -- is written into Y, so each level costs
 // ONE workgroup barrier.  With one buffer (long signals), a second barrier guards the overwrite.
-template <typename T, int L, bool FMA, int NV, bool VALIDATE>
+// Non-finite probe (VW_FLAG_REF_NONFINITE, vw_ref.hip): z = v * 0 + z stays +-0 while every v is finite
+// and becomes NaN for good at the first NaN / +-Inf -- one FMA per value, no compare or mask in the loop.
+template <typename T, int V>
+__device__ __forceinline__ void nf_probe(T& z, const T (&v)[V]) {
+#pragma unroll
+  for (int e = 0; e < V; ++e) {
+    if constexpr (sizeof(T) == 8) z = __builtin_fma(v[e], T(0), z);
+    else z = __builtin_fmaf(v[e], T(0), z);
+  }
+}
+// a row in registers (load_row_regs layout): only the vectors the thread holds (for_vecs)
+template <typename T, int L, int NV, int V>
+__device__ __forceinline__ void nf_probe_rows(T& z, const T (&v)[NV][V], int nvec) {
+  for_vecs<L, NV>(nvec, [&](int k, int) { nf_probe<T, V>(z, v[k]); });
+}
+// row b flagged when any lane of any wave saw one (a plain vector store: every writer stores the same 1)
+template <typename T>
+__device__ __forceinline__ void nf_flag_row(int* flag, long long b, T z) {
+  if (__any(z != z) && (threadIdx.x & 63) == 0) flag[b] = 1;
+}
+
+// NFP: probe the details (nf: the row's accumulator, see nf_probe)
+template <typename T, int L, bool FMA, int NV, bool VALIDATE, bool NFP = false>
 __device__ __forceinline__ void fwd_level(const FwdArgs<T>& p, const T* X, int nvec, const LevelDesc& lv, T* dout,
-                                          T* aout, bool vec_ok, unsigned long long flat0, T (&areg)[NV][VT<T>::V]) {
+                                          T* aout, bool vec_ok, unsigned long long flat0, T (&areg)[NV][VT<T>::V],
+                                          T* nf = nullptr) {
   constexpr int V = VT<T>::V;
   const int N = p.N;
   fwd_row<T, L, FMA, NV>(X, nvec, lv.s, p.lo, p.hi, p.taps, [&](int k, int w, const T (&al)[V], const T (&ah)[V]) {
@@ -741,6 +764,7 @@ __device__ __forceinline__ void fwd_level(const FwdArgs<T>& p, const T* X, int n
       check_out<T>(1, p.bad, flat0, t0, N, ah);
       check_out<T>(1, p.bad, flat0, t0, N, al);
     }
+    if constexpr (NFP) nf_probe<T, V>(*nf, ah);  // the details suffice (k_forward_persist)
 #pragma unroll
     for (int e = 0; e < V; ++e) areg[k][e] = al[e];
   });
@@ -946,6 +970,7 @@ k_forward_persist(const FwdArgs<T> p) {
   long long b = blockIdx.x;
   if (b >= p.B) return;
   int cur = 0;
+  T nf = T(0);
   dma_row<T>(B0, p.x + b * p.ldx, nvec, p.dma_nt != 0);
   wait_vmem();
   for (;;) {
@@ -964,11 +989,20 @@ k_forward_persist(const FwdArgs<T> p) {
       }
       T* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
       T* aout = (j == p.J) ? p.approx + b * (size_t)N : nullptr;
-      fwd_level<T, L, FMA, NV, false>(p, X, nvec, lv, dout, aout, true, 0ull, areg);
+      if (p.nf_flag) fwd_level<T, L, FMA, NV, false, true>(p, X, nvec, lv, dout, aout, true, 0ull, areg, &nf);
+      else fwd_level<T, L, FMA, NV, false>(p, X, nvec, lv, dout, aout, true, 0ull, areg);
       if (j < p.J) {
         regs_to_level<T, L, NV>(Y, areg, nvec, N, p.lv[j], p.npow2, (const T*)nullptr);
         T* t = X; X = Y; Y = t;
       }
+    }
+    // VW_FLAG_REF_NONFINITE: the reference differs only where a level input (x, a_1 .. a_{J-1}) holds a
+    // NaN / +-Inf; such a value reaches that level's details through the non-zero high-pass taps (and a
+    // non-finite a_J is identical in both), so probing the details flags exactly the rows vw_ref.hip must
+    // recompute (an overflow to Inf in a detail sum adds a harmless recompute)
+    if (p.nf_flag) {
+      nf_flag_row<T>(p.nf_flag, b, nf);
+      nf = T(0);
     }
     if (bn >= p.B) break;
     wait_vmcnt<2 * NV>();  // this wave's DMA share landed; level J's stores stay in flight
@@ -1105,6 +1139,11 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, VW_INV_W)) k_inverse_seq(const
 
   T acc[NV][V];
   T dreg[NV][V];
+  // VW_FLAG_REF_NONFINITE: a NaN / +-Inf in any level input (a_J, a d_j the threshold keeps, an
+  // intermediate approximation) reaches y through the non-zero taps (0 * Inf never occurs in these sums),
+  // so probing y flags exactly the rows vw_ref.hip must recompute
+  T nf = T(0);
+  const bool nfp = p.nf_flag != nullptr;
   load_row_regs<T, NV>(acc, p.approx + b * (size_t)N, N, nvec, vec_ok, p.approx_zero != 0);
   load_row_regs<T, NV>(dreg, p.details + (size_t)(p.J - 1) * plane + b * (size_t)N, N, nvec, vec_ok,
                        p.lv[p.J - 1].use_d == 0);
@@ -1138,6 +1177,10 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, VW_INV_W)) k_inverse_seq(const
     }
   }
   for_vecs<L, NV>(nvec, [&](int k, int w) { store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, w * V, N, vec_ok, acc[k]); });
+  if (nfp) {
+    nf_probe_rows<T, L, NV, V>(nf, acc, nvec);
+    nf_flag_row<T>(p.nf_flag, b, nf);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------

@@ -65,6 +65,8 @@ struct FwdArgs {
   int taps;             // L (runtime copy; kernels are also templated on it)
   int tap_lds;          // k_forward_blk: element offset of the LDS tap table
   int blk_tight;        // k_forward_blk: sparse padding (blk_layout)
+  int* nf_flag;         // k_forward_persist, VW_FLAG_REF_NONFINITE: nf_flag[b] = 1 when an output of row b is
+                        // non-finite (nullptr = off; the rows vw_ref.hip recomputes)
   T lo[kMaxTaps];       // base taps * 1/sqrt(2)  (ScalarOps.java:909-916: same at every level)
   T hi[kMaxTaps];
   LevelDesc lv[kMaxLevels];
@@ -93,6 +95,8 @@ struct InvArgs {
   int taps;
   int tap_lds;          // k_inverse_blk: element offset of the LDS tap table
   int blk_tight;        // k_inverse_blk: sparse padding (blk_layout)
+  int* nf_flag;         // k_inverse_seq, VW_FLAG_REF_NONFINITE: nf_flag[b] = 1 when an input or the output of
+                        // row b is non-finite (nullptr = off)
   T lo[kMaxTaps];
   T hi[kMaxTaps];
   LevelDesc lv[kMaxLevels];
@@ -189,7 +193,7 @@ struct RefScan {                // flag[b] = 1 when row b of any plane is non-fi
   long long B;
   int N;
   int chunks;                   // ref_scan_chunks(N)
-  int* flag;                    // [B], zeroed by the caller
+  int* flag;                    // [B], kept zero between calls (k_ref_* clear the rows they recompute)
 };
 template <typename T>
 struct RefArgs {
@@ -207,7 +211,7 @@ struct RefArgs {
   int J;
   int L;
   int mode;                     // kHaloPeriodic / kHaloZero / kHaloSymmetric
-  const int* flag;              // rows to recompute
+  int* flag;                    // rows to recompute (cleared once recomputed)
   T* scratch;                   // [grid][2][N] running approximations
   T lo[kMaxTaps];               // base taps * 1/sqrt(2), as the fast kernels
   T hi[kMaxTaps];

@@ -18,7 +18,10 @@
 // zeros included, separate multiply and add in the reference's order -- bit-identical to it, NaN and
 // +-Inf included.  Flagged rows are rare (they are invalid input to every validated entry point), so
 // this is one persistent launch of one workgroup per row, reading the level input from global memory
-// (L2); a call with no flagged row pays one scan of its planes and an empty launch.
+// (L2); a call with no flagged row pays one scan of its planes and an empty launch.  The headline
+// kernels (k_forward_persist, k_inverse_seq) flag their rows themselves (FwdArgs / InvArgs nf_flag: one
+// FMA per value, v * 0 + z is NaN iff v is not finite) and the scan is skipped.  Flags stay zero
+// between calls: these kernels clear every row they recompute.
 #include <hip/hip_runtime.h>
 #include "vw_internal.h"
 
@@ -107,6 +110,7 @@ __global__ void __launch_bounds__(512) k_ref_forward(RefArgs<T> a) {
       __syncthreads();  // the level's approximation is the next level's input (same workgroup, same CU)
       cur = out_a;
     }
+    if (threadIdx.x == 0) a.flag[b] = 0;  // read by every thread before the levels' barriers
   }
 }
 
@@ -170,6 +174,7 @@ __global__ void __launch_bounds__(512) k_ref_inverse(RefArgs<T> a) {
       __syncthreads();
       cur = out;
     }
+    if (threadIdx.x == 0) a.flag[b] = 0;
   }
 }
 
