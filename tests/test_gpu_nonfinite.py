@@ -236,3 +236,81 @@ def test_headline_kernels_flag_their_own_rows(engine):
     y3 = engine.inverse(d3, a3, lr, hr, w.wavelet_id, O.PERIODIC, J, F)
     assert torch.equal(d2.view(torch.int64), d3.view(torch.int64)) and torch.equal(a2.view(torch.int64), a3.view(torch.int64))
     assert torch.equal(y2.view(torch.int64), y3.view(torch.int64))
+
+
+def test_ref_nonfinite_in_a_captured_graph(engine):
+    # the row flags are allocated by the first call and cleared by the fix-up kernels, so a recorded
+    # forward + inverse with VW_FLAG_REF_NONFINITE replays correctly whether or not a replay meets a NaN
+    import torch
+    from ctypes import c_void_p
+    from vectorwave_amd import _native as nat
+    w, B, N, J = Daubechies.DB4, 640, 4096, 6
+    F = nat.FLAG_FMA | nat.FLAG_REF_NONFINITE
+    lo, hi = nat.taps_array(w.lowPassDecomposition()), nat.taps_array(w.highPassDecomposition())
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        x = torch.empty((B, N), dtype=torch.float64, device="cuda")
+        det = torch.empty((J, B, N), dtype=torch.float64, device="cuda")
+        app, y = torch.empty_like(x), torch.empty_like(x)
+        engine.fill_uniform(x, 7)
+        lib, ctx = engine.lib, engine.ctx
+        P = lambda t: c_void_p(t.data_ptr())  # noqa: E731
+
+        def step():
+            assert lib.vw_modwt_forward_f64(ctx, P(x), B, N, N, lo, hi, len(lo), w.wavelet_id, 0, J, F,
+                                            P(det), P(app)) == 0
+            assert lib.vw_modwt_inverse_f64(ctx, P(det), P(app), B, N, lo, hi, len(lo), w.wavelet_id, 0, J,
+                                            0xFFFFFFFF, 0, F, P(y)) == 0
+
+        step()
+        torch.cuda.synchronize()
+        d0, a0, y0 = det.clone(), app.clone(), y.clone()
+        g = engine.capture(step)
+        x[411, 1000] = float("nan")
+        g.launch(1)
+        torch.cuda.synchronize()
+        xh = x.cpu().numpy()
+        d_ref, a_ref = O.decompose(xh[411], w.lowPassDecomposition(), w.highPassDecomposition(), O.PERIODIC, J,
+                                   core=False)
+        same(det[:, 411].cpu().numpy(), d_ref, "replayed details row 411")
+        same(app[411].cpu().numpy(), a_ref, "replayed approx row 411")
+        same(y[411].cpu().numpy(), O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(),
+                                                 O.PERIODIC), "replayed inverse row 411")
+        engine.fill_uniform(x, 7)  # the clean input again
+        g.launch(2)
+        torch.cuda.synchronize()
+        assert torch.equal(det.view(torch.int64), d0.view(torch.int64))
+        assert torch.equal(app.view(torch.int64), a0.view(torch.int64))
+        assert torch.equal(y.view(torch.int64), y0.view(torch.int64))
+        g.close()
+
+
+def test_ref_nonfinite_fp32_headline_kernels(engine):
+    # the fp32 persistent forward / sequential inverse probe their rows too; the reference has no fp32 path,
+    # so the bar is the fp64 restatement's NaN / +-Inf positions and the FMA path's fp32 tolerance elsewhere
+    import torch
+    from vectorwave_amd import _native as nat
+    w, n, J, B = Daubechies.DB4, 4096, 6, 640
+    x = O.fill_uniform(B * n, 31).reshape(B, n).astype(np.float32)
+    x[5, 77] = np.nan
+    x[600, 4000] = -np.inf
+    lo, hi = lohi(w)
+    lr, hr = w.lowPassReconstruction(), w.highPassReconstruction()
+    xt = torch.from_numpy(x).cuda()
+    d, a = engine.forward(xt, lo, hi, w.wavelet_id, O.PERIODIC, J, nat.FLAG_FMA | nat.FLAG_REF_NONFINITE)
+    y = engine.inverse(d, a, lr, hr, w.wavelet_id, O.PERIODIC, J, nat.FLAG_FMA | nat.FLAG_REF_NONFINITE)
+    d0, a0 = engine.forward(xt, lo, hi, w.wavelet_id, O.PERIODIC, J, nat.FLAG_FMA)
+    d, a, y = d.cpu().numpy(), a.cpu().numpy(), y.cpu().numpy()
+    tol = 1e-5 * J
+    for b in (5, 600):
+        d_ref, a_ref = O.decompose(x[b].astype(np.float64), lo, hi, O.PERIODIC, J, core=False)
+        y_ref = O.reconstruct(d_ref, a_ref, lr, hr, O.PERIODIC)
+        for got, ref, what in ((d[:, b, :], d_ref, "details"), (a[b], a_ref, "approx"), (y[b], y_ref, "y")):
+            assert np.array_equal(np.isnan(got), np.isnan(ref)), (b, what)
+            assert np.array_equal(np.isposinf(got), np.isposinf(ref)) and np.array_equal(np.isneginf(got),
+                                                                                         np.isneginf(ref)), (b, what)
+            f = np.isfinite(ref)
+            assert np.max(np.abs(got[f] - ref[f]), initial=0.0) <= tol, (b, what)
+    clean = np.setdiff1d(np.arange(B), [5, 600])
+    assert np.array_equal(d[:, clean, :], d0.cpu().numpy()[:, clean, :])
+    assert np.array_equal(a[clean], a0.cpu().numpy()[clean])
