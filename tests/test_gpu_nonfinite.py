@@ -314,3 +314,27 @@ def test_ref_nonfinite_fp32_headline_kernels(engine):
     clean = np.setdiff1d(np.arange(B), [5, 600])
     assert np.array_equal(d[:, clean, :], d0.cpu().numpy()[:, clean, :])
     assert np.array_equal(a[clean], a0.cpu().numpy()[clean])
+
+
+@pytest.mark.parametrize("boundary", [O.PERIODIC, O.SYMMETRIC], ids=["P", "S"])
+def test_swt_full_batch_rows_probe_themselves(engine, boundary):
+    # 640 rows (> 2 per CU): the kernels that probe their own rows (persistent forward; one-buffer sequential
+    # inverse for the K6 symmetric reconstruction) instead of the scan pass
+    w, n, J, B = Daubechies.DB4, 4096, 4, 640
+    x = O.fill_uniform(B * n, 13).reshape(B, n)
+    x[3, 0] = np.nan
+    x[320, 2047] = np.inf
+    x[B - 1, n - 1] = -np.inf
+    swt = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode(boundary))
+    res = swt.forward(x, J)
+    y = swt.inverse(res)
+    for b in (3, 4, 320, B - 1):
+        d_ref, a_ref = O.swt_forward(x[b], *lohi(w), boundary, J)
+        same(res.details_array[:, b, :], d_ref, f"details row {b}")
+        same(res.approximation_array[b], a_ref, f"approx row {b}")
+        if boundary == O.PERIODIC:
+            y_ref = O.swt_reconstruct_periodic(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction())
+        else:
+            y_ref = O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(), boundary,
+                                  wavelet_id=w.wavelet_id)
+        same(y[b], y_ref, f"inverse row {b}")
