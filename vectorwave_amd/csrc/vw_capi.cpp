@@ -1348,10 +1348,12 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
       bool ok = (tu.mfma & 1) && fma && !single_level && a.vec_io && !validate && !hist && mfma_supported(L, N);
       for (int j = 0; ok && j < J; ++j) ok = lv[j].mode == kHaloPeriodic;
       const int H = ok ? mfma_halo(L, J) : 0;
-      if (ok && H <= N && (int64_t)(N + H + 2 * L) * 4 <= kLdsBytes) {
+      const int region = ok ? mfma_region((int)N + H) : 0;  // padded LDS layout (vw_mfma.hip ph)
+      const int scratch = 8 * 256 + 4;  // the forward's per-wave transpose scratch (<= 8 waves), aligned
+      if (ok && H <= N && (int64_t)(region + 2 * L + scratch) * 4 <= kLdsBytes) {
         a.hlpad = H;
-        a.tap_lds = (int)N + H;
-        mfma_lds = (int)((N + H + 2 * L) * 4);
+        a.tap_lds = region;
+        mfma_lds = (int)((region + 2 * L + scratch) * 4);
       }
     }
     // VW_FLAG_REF_NONFINITE: the persistent forward probes its own outputs (no scan pass afterwards)
@@ -1630,10 +1632,11 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
       bool ok = (tu.mfma & 2) && fma && !pair && boundary == VW_PERIODIC && a.vec_io && mfma_supported(L, N);
       for (int j = 0; ok && j < J; ++j) ok = lv[j].dir_a == 1 && lv[j].dir_d == 1 && lv[j].off_a == 0 && lv[j].off_d == 0;
       const int H = ok ? mfma_halo(L, J) : 0;
-      if (ok && H <= N && (int64_t)(N + H + 2 * L) * 4 <= kLdsBytes) {
+      const int region = ok ? mfma_region((int)N + H) : 0;
+      if (ok && H <= N && (int64_t)(region + 2 * L) * 4 <= kLdsBytes) {
         a.hlpad_a = H;
-        a.tap_lds = (int)N + H;
-        mfma_lds = (int)((N + H + 2 * L) * 4);
+        a.tap_lds = region;
+        mfma_lds = (int)((region + 2 * L) * 4);
       }
     }
     // VW_FLAG_REF_NONFINITE: the one-buffer sequential kernel (vw_inv.hip's choice) probes its inputs and

@@ -226,6 +226,7 @@ int ref_scan_chunks(int N);
 // Matrix-core fp32 kernels (vw_mfma.hip): which (L, N) are instantiated, the halo a level set needs, launchers.
 bool mfma_supported(int L, long long N);
 int mfma_halo(int L, int J);
+int mfma_region(int n);  // LDS floats of the kernels' padded level region for elements [0, n)
 hipError_t launch_forward_mfma(const FwdArgs<float>& a, int lds, hipStream_t st);
 hipError_t launch_inverse_mfma(const InvArgs<float>& a, int lds, hipStream_t st);
 

@@ -25,7 +25,7 @@
 // consecutive residues of group g, class block cb).  Lane l holds O[4*(l>>4) + v][l & 15], v = 0..3.
 //
 // Scope: PERIODIC, fp32, VW_FLAG_FMA (EXACT keeps the VALU kernels: separate multiply and add), one signal
-// per 256-thread workgroup, N = 1024 * TPW samples (TPW tiles per wave), every level's halo (4*KS - 16)*s
+// per workgroup (NT threads, N = 4 * NT * TPW samples, TPW tiles per wave), every level's halo (4*KS - 16)*s
 // within the row.  Host policy: vw_capi.cpp (VW_MFMA).
 #include "vw_device.h"
 
@@ -57,29 +57,76 @@ __device__ __forceinline__ void store4(float* __restrict__ row, int t, int s, f4
   }
 }
 
-constexpr int kMfmaThreads = 256;
+// A tile's four outputs per lane (t = base + s*(4*kk + v)) to a row: s = 1 one 16-byte store; 2 <= s < 16
+// through the wave's scratch (sc, 256 floats) so that lane l stores samples 256*tile + 4l .. 4l+3; s >= 16
+// four scattered stores (16 consecutive residues: 64-byte pieces).
+__device__ __forceinline__ void put_tile(float* sc, int lane, float* __restrict__ row, int tile, int t, int s, f4 v) {
+  if (s == 1) {
+    __builtin_nontemporal_store(v, reinterpret_cast<f4*>(row + t));
+  } else if (s < 16) {
+    const int o = t - 256 * tile;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) sc[o + e * s] = v[e];
+    __builtin_amdgcn_wave_barrier();  // one wave's LDS accesses run in order; keep the compiler's order too
+    const f4 w = *reinterpret_cast<const f4*>(sc + 4 * lane);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_nontemporal_store(w, reinterpret_cast<f4*>(row + 256 * tile + 4 * lane));
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) row[t + e * s] = v[e];
+  }
+}
+
+// Workgroup: NT threads (NT / 64 waves of TPW tiles each, N = 4 * NT * TPW).  N = 8192 runs 512 threads of
+// four tiles (the inverse's registers at eight tiles per wave -- its row prefetch alone is 2 x 32 VGPRs --
+// left two waves per SIMD); VW_MFMA_NT8K=256 restores one workgroup of 256 threads x 8 tiles.
+#ifndef VW_MFMA_NT8K
+#define VW_MFMA_NT8K 512
+#endif
+
+// LDS layout: element i at slot ph(i) = i + (i >> S), one pad per 2^S elements (S = 3 by default).  The 16
+// columns of a tile sit 16*s elements apart, i.e. on 2 of a half wave's 32 banks unpadded (8-way at s = 1, 2);
+// padded, the modelled B reads are conflict-free at s <= 4 and 2-way above, and -- what keeps them one
+// ds_read at an offset -- the slot distance ph(i0 -+ 4*s*q) - ph(i0) of k-step q is the same for every lane
+// and tile of a level (dq below, computed once per level).
+#ifndef VW_MFMA_PAD_SHIFT
+#define VW_MFMA_PAD_SHIFT 3
+#endif
+__device__ __forceinline__ int ph(int i) { return i + (i >> VW_MFMA_PAD_SHIFT); }
 
 // Forward, PERIODIC, fp32 FMA: all J levels of one signal per workgroup.  One LDS level buffer X: element t
 // at X[H + t] for t in [-H, N) (left wrap images; H = p.hlpad >= (4*KS - 16) * s_J); taps at p.tap_lds.
 // Per level: every tile of the wave computed (approximations kept in registers, details stored), barrier,
-// approximations written back as the next level's input, barrier.
-template <int L, int TPW>
-__global__ void __launch_bounds__(kMfmaThreads) k_forward_mfma(const FwdArgs<float> p) {
+// approximations written back as the next level's input, barrier.  (Two level buffers -- write-back straight
+// after each tile pair, one barrier per level -- measured slower: one 1024-thread workgroup per CU,
+// profiles/r06/ab_coif5_mfma_v3_two_level_buffers.log.)
+template <int L, int TPW, int NT>
+__global__ void __launch_bounds__(NT) k_forward_mfma(const FwdArgs<float> p) {
   constexpr int KS = (L + 15 + 3) / 4;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* X = reinterpret_cast<float*>(smem);
-  float* taps = X + p.tap_lds;
+  float* taps = reinterpret_cast<float*>(smem) + p.tap_lds;
+  // per-wave transpose scratch (256 floats after the taps): at 2 <= s < 16 a tile is the 256 consecutive
+  // samples [256*tile, +256) in the MFMA's lane order, four per lane s apart; through the scratch every lane
+  // stores 16 contiguous bytes (whole lines) instead of four scattered floats
+  float* const SC = reinterpret_cast<float*>(smem) + ((p.tap_lds + 2 * L + 3) & ~3) + 256 * (threadIdx.x >> 6);
   const int N = p.N, H = p.hlpad;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int row = lane & 15, kk = lane >> 4;
   const long long b = blockIdx.x;
-  for (int i = tid; i < 2 * L; i += kMfmaThreads) taps[i] = i < L ? p.lo[i] : p.hi[i - L];
+  for (int i = tid; i < 2 * L; i += NT) taps[i] = i < L ? p.lo[i] : p.hi[i - L];
   {
     const f4* xr = reinterpret_cast<const f4*>(p.x + b * p.ldx);
-    for (int w = tid; w < N / 4; w += kMfmaThreads) {
+    for (int w = tid; w < N / 4; w += NT) {
       const f4 v = __builtin_nontemporal_load(xr + w);
-      *reinterpret_cast<f4*>(X + H + 4 * w) = v;
-      if (4 * w >= N - H) *reinterpret_cast<f4*>(X + H + 4 * w - N) = v;
+      const int o = ph(H + 4 * w);  // an aligned 4-group stays contiguous (pads fall between 8-groups)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) X[o + e] = v[e];
+      if (4 * w >= N - H) {
+        const int oi = ph(H + 4 * w - N);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) X[oi + e] = v[e];
+      }
     }
   }
   __syncthreads();
@@ -94,6 +141,13 @@ __global__ void __launch_bounds__(kMfmaThreads) k_forward_mfma(const FwdArgs<flo
   for (int j = 1; j <= p.J; ++j) {
     const int s = 1 << (j - 1);
     const bool last = j == p.J;
+    const unsigned xb = lds_base(X);
+    int dq[KS];  // slot distance of k-step q (lane- and tile-uniform)
+    {
+      const int r0 = H + mfma_base(0, s, 0) + 15 * s;
+#pragma unroll
+      for (int q = 0; q < KS; ++q) dq[q] = ph(r0 - 4 * s * q) - ph(r0);
+    }
     float* dout = p.details + ((size_t)(j - 1) * (size_t)p.B + (size_t)b) * (size_t)N;
     float* aout = p.approx + b * (size_t)N;
     f4 keep[TPW];
@@ -108,9 +162,9 @@ __global__ void __launch_bounds__(kMfmaThreads) k_forward_mfma(const FwdArgs<flo
       for (int h = 0; h < 2; ++h) {
         base[h] = mfma_base(wave * TPW + i + h, s, row);
         // B operand of k-step q: X[k = 4q + kk][n] = x[base + s*(15 - 4q - kk)]
-        const unsigned a0 = lds_base(X + H + base[h] + s * (15 - kk));
+        const unsigned a0 = xb + 4u * (unsigned)ph(H + base[h] + s * (15 - kk));
 #pragma unroll
-        for (int q = 0; q < KS; ++q) xv[h][q] = lds_vec_at<float>(a0 - (unsigned)(16 * s * q));
+        for (int q = 0; q < KS; ++q) xv[h][q] = lds_vec_at<float>(a0 + 4u * (unsigned)dq[q]);
       }
       __builtin_amdgcn_sched_barrier(0);
       f4 lo[2] = {}, hi[2] = {};
@@ -124,8 +178,9 @@ __global__ void __launch_bounds__(kMfmaThreads) k_forward_mfma(const FwdArgs<flo
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int t = base[h] + 4 * s * kk;  // this lane's outputs: t + s*v
-        store4(dout, t, s, hi[h]);
-        if (last) store4(aout, t, s, lo[h]);
+        const int tile = wave * TPW + i + h;
+        put_tile(SC, lane, dout, tile, t, s, hi[h]);
+        if (last) put_tile(SC, lane, aout, tile, t, s, lo[h]);
         keep[i + h] = lo[h];
       }
     }
@@ -137,8 +192,8 @@ __global__ void __launch_bounds__(kMfmaThreads) k_forward_mfma(const FwdArgs<flo
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int te = t + e * s;
-        X[H + te] = keep[i][e];
-        if (te >= N - H) X[H + te - N] = keep[i][e];
+        X[ph(H + te)] = keep[i][e];
+        if (te >= N - H) X[ph(H + te - N)] = keep[i][e];
       }
     }
     __syncthreads();
@@ -149,8 +204,8 @@ __global__ void __launch_bounds__(kMfmaThreads) k_forward_mfma(const FwdArgs<flo
 // accumulator per output), fp32 FMA.  One LDS region R time-shared by a_j and d_j: element t at R[t] for t in
 // [0, N + H) (right wrap images, H = p.hlpad_a >= (4*KS - 16) * s_J); the tiles' accumulators stay in
 // registers across the swap; d_{j-1} is prefetched into registers while level j computes.
-template <int L, int TPW>
-__global__ void __launch_bounds__(kMfmaThreads) k_inverse_mfma(const InvArgs<float> p) {
+template <int L, int TPW, int NT>
+__global__ void __launch_bounds__(NT) k_inverse_mfma(const InvArgs<float> p) {
   constexpr int KS = (L + 15 + 3) / 4;
   constexpr int RV = TPW;  // float4 row vectors per thread: N / 4 / 256 = TPW
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -161,25 +216,32 @@ __global__ void __launch_bounds__(kMfmaThreads) k_inverse_mfma(const InvArgs<flo
   const int row = lane & 15, kk = lane >> 4;
   const long long b = p.rev ? p.B - 1 - (long long)blockIdx.x : (long long)blockIdx.x;
   const size_t plane = (size_t)p.B * (size_t)N;
-  for (int i = tid; i < 2 * L; i += kMfmaThreads) taps[i] = i < L ? p.lo[i] : p.hi[i - L];
+  const unsigned rb = lds_base(R);
+  for (int i = tid; i < 2 * L; i += NT) taps[i] = i < L ? p.lo[i] : p.hi[i - L];
   // a row (standard mapping: vector tid + k*256) into R with the right images of the level's reach
   auto stage = [&](const f4 (&r)[RV], int reach, int mode, float thr) {
 #pragma unroll
     for (int k = 0; k < RV; ++k) {
-      const int t = 4 * (tid + k * kMfmaThreads);
+      const int t = 4 * (tid + k * NT);
       f4 v = r[k];
       if (mode == 1) v = f4{0.f, 0.f, 0.f, 0.f};
       if (mode == 2) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = threshold_t(v[e], thr, p.soft);
       }
-      *reinterpret_cast<f4*>(R + t) = v;
-      if (t < reach) *reinterpret_cast<f4*>(R + N + t) = v;
+      const int o = ph(t);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) R[o + e] = v[e];
+      if (t < reach) {
+        const int oi = ph(N + t);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) R[oi + e] = v[e];
+      }
     }
   };
   auto load = [&](f4 (&r)[RV], const float* src) {
 #pragma unroll
-    for (int k = 0; k < RV; ++k) r[k] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src) + tid + k * kMfmaThreads);
+    for (int k = 0; k < RV; ++k) r[k] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(src) + tid + k * NT);
   };
   auto reach_of = [&](int j) { return (4 * KS - 16) << (j - 1); };
   auto thr_of = [&](int j) { return p.thr ? load_uniform(p.thr + (size_t)(j - 1) * (size_t)p.thr_ld + (size_t)b) : 0.f; };
@@ -199,6 +261,12 @@ __global__ void __launch_bounds__(kMfmaThreads) k_inverse_mfma(const InvArgs<flo
   for (int j = p.J; j >= 1; --j) {
     const int s = 1 << (j - 1);
     const LevelDesc& lv = p.lv[j - 1];
+    int dq[KS];  // slot distance of k-step q (lane- and tile-uniform)
+    {
+      const int r0 = mfma_base(0, s, 0);
+#pragma unroll
+      for (int q = 0; q < KS; ++q) dq[q] = ph(r0 + 4 * s * q) - ph(r0);
+    }
     __syncthreads();  // R = a_j + images
     f4 acc[TPW];
     // one branch over the wave's tiles, two at a time: B values first, then two interleaved chains
@@ -208,9 +276,9 @@ __global__ void __launch_bounds__(kMfmaThreads) k_inverse_mfma(const InvArgs<flo
         float xv[2][KS];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          const unsigned a0 = lds_base(R + mfma_base(wave * TPW + i + h, s, row) + s * kk);
+          const unsigned a0 = rb + 4u * (unsigned)ph(mfma_base(wave * TPW + i + h, s, row) + s * kk);
 #pragma unroll
-          for (int q = 0; q < KS; ++q) xv[h][q] = lds_vec_at<float>(a0 + (unsigned)(16 * s * q));
+          for (int q = 0; q < KS; ++q) xv[h][q] = lds_vec_at<float>(a0 + 4u * (unsigned)dq[q]);
         }
         __builtin_amdgcn_sched_barrier(0);
         f4 c[2];
@@ -244,8 +312,8 @@ __global__ void __launch_bounds__(kMfmaThreads) k_inverse_mfma(const InvArgs<flo
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int te = t + e * s;
-        R[te] = acc[i][e];
-        if (te < reach) R[N + te] = acc[i][e];
+        R[ph(te)] = acc[i][e];
+        if (te < reach) R[ph(N + te)] = acc[i][e];
       }
     }
   }
@@ -253,34 +321,34 @@ __global__ void __launch_bounds__(kMfmaThreads) k_inverse_mfma(const InvArgs<flo
 
 // Host side: FwdArgs / InvArgs as the fused kernels; p.hlpad (forward) / p.hlpad_a (inverse) = the halo,
 // p.tap_lds = the tap table's element offset.  L = 30 (coif5) and 16 (db8 / sym8) are instantiated.
-template <int L, int TPW>
+template <int L, int TPW, int NT>
 static hipError_t run_fwd(const FwdArgs<float>& a, int lds, hipStream_t st) {
-  auto k = k_forward_mfma<L, TPW>;
+  auto k = k_forward_mfma<L, TPW, NT>;
   static LdsOnce configured;
   hipError_t e = set_lds(k, lds, &configured);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(kMfmaThreads), lds, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(NT), lds, st, a);
   return hipGetLastError();
 }
 
-template <int L, int TPW>
+template <int L, int TPW, int NT>
 static hipError_t run_inv(const InvArgs<float>& a, int lds, hipStream_t st) {
-  auto k = k_inverse_mfma<L, TPW>;
+  auto k = k_inverse_mfma<L, TPW, NT>;
   static LdsOnce configured;
   hipError_t e = set_lds(k, lds, &configured);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(kMfmaThreads), lds, st, a);
+  hipLaunchKernelGGL(k, dim3((unsigned)a.B), dim3(NT), lds, st, a);
   return hipGetLastError();
 }
 
 #define VW_MFMA_DISPATCH(RUN, a, lds, st)                                    \
   switch (a.taps * 100 + a.N / 1024) {                                       \
-    case 3002: return RUN<30, 2>(a, lds, st);                                \
-    case 3004: return RUN<30, 4>(a, lds, st);                                \
-    case 3008: return RUN<30, 8>(a, lds, st);                                \
-    case 1602: return RUN<16, 2>(a, lds, st);                                \
-    case 1604: return RUN<16, 4>(a, lds, st);                                \
-    case 1608: return RUN<16, 8>(a, lds, st);                                \
+    case 3002: return RUN<30, 2, 256>(a, lds, st);                           \
+    case 3004: return RUN<30, 4, 256>(a, lds, st);                           \
+    case 3008: return RUN<30, 8192 / 4 / VW_MFMA_NT8K, VW_MFMA_NT8K>(a, lds, st); \
+    case 1602: return RUN<16, 2, 256>(a, lds, st);                           \
+    case 1604: return RUN<16, 4, 256>(a, lds, st);                           \
+    case 1608: return RUN<16, 8192 / 4 / VW_MFMA_NT8K, VW_MFMA_NT8K>(a, lds, st); \
     default: return hipErrorNotSupported;                                    \
   }
 
@@ -289,6 +357,9 @@ bool mfma_supported(int L, long long N) {
 }
 
 int mfma_halo(int L, int J) { return (4 * ((L + 15 + 3) / 4) - 16) << (J - 1); }
+
+// LDS floats of the padded level region of elements [0, n) (the tap table follows it)
+int mfma_region(int n) { return n == 0 ? 0 : (n - 1) + ((n - 1) >> VW_MFMA_PAD_SHIFT) + 1; }
 
 hipError_t launch_forward_mfma(const FwdArgs<float>& a, int lds, hipStream_t st) { VW_MFMA_DISPATCH(run_fwd, a, lds, st) }
 hipError_t launch_inverse_mfma(const InvArgs<float>& a, int lds, hipStream_t st) { VW_MFMA_DISPATCH(run_inv, a, lds, st) }
