@@ -64,14 +64,16 @@ __global__ void __launch_bounds__(512) fanin(const double* __restrict__ in, doub
 int main(int argc, char** argv) {
   const int B = 4096, N = 4096, J = 7, R = 4, K = 20, WARM = 40;
   const long long plane = (long long)B * N;
+  // ./stepbench S LDS_FWD LDS_INV STAGGER: coefficient planes STAGGER doubles apart beyond B*N (0: contiguous)
+  const long long pstr = plane + (argc > 4 ? atoll(argv[4]) : 0);
   struct Set { double *x, *c, *y; };
   std::vector<Set> sets(R);
   for (auto& s : sets) {
     CHK(hipMalloc(&s.x, plane * 8));
-    CHK(hipMalloc(&s.c, plane * 8 * J));
+    CHK(hipMalloc(&s.c, pstr * 8 * J));
     CHK(hipMalloc(&s.y, plane * 8));
     CHK(hipMemset(s.x, 0, plane * 8));
-    CHK(hipMemset(s.c, 0, plane * 8 * J));
+    CHK(hipMemset(s.c, 0, pstr * 8 * J));
   }
   const double step_bytes = plane * 8.0 * 16;  // 1 + 7 planes forward, 7 + 1 inverse
   int smax = argc > 1 ? atoi(argv[1]) : 4;
@@ -97,7 +99,7 @@ int main(int argc, char** argv) {
         for (int p = 0; p < S; ++p) {
           const long long rows = B / S, r0 = p * rows;
           fwd(s, rows, r0, st[p]);
-          hipLaunchKernelGGL(fanin, dim3((unsigned)rows), dim3(512), 0, st[p], s.c, s.y, N, plane, J, r0);
+          hipLaunchKernelGGL(fanin, dim3((unsigned)rows), dim3(512), 0, st[p], s.c, s.y, N, pstr, J, r0);
         }
       }
     };
@@ -129,8 +131,8 @@ int main(int argc, char** argv) {
       for (int i = 0; i < K; ++i) {
         const Set& s = sets[i % R];
         const long long rows = B / S, r0 = p * rows;
-        hipLaunchKernelGGL(fanout<16>, dim3((unsigned)rows), dim3(512), lds_f, st[p], s.x, s.c, N, plane, J, r0);
-        hipLaunchKernelGGL(fanin, dim3((unsigned)rows), dim3(512), lds_i, st[p], s.c, s.y, N, plane, J, r0);
+        hipLaunchKernelGGL(fanout<16>, dim3((unsigned)rows), dim3(512), lds_f, st[p], s.x, s.c, N, pstr, J, r0);
+        hipLaunchKernelGGL(fanin, dim3((unsigned)rows), dim3(512), lds_i, st[p], s.c, s.y, N, pstr, J, r0);
       }
       hipGraph_t g;
       CHK(hipStreamEndCapture(st[p], &g));
@@ -153,38 +155,39 @@ int main(int argc, char** argv) {
       float ms = 0;
       CHK(hipEventElapsedTime(&ms, e0, e1));
       const double per = ms / K;
-      printf("{\"pattern\": \"the step, one graph per stream\", \"lds_fwd\": %d, \"lds_inv\": %d, \"streams\": %d, "
-             "\"rep\": %d, \"ms_per_step\": %.4f, \"Msamples_per_s\": %.1f, \"GBps\": %.1f}\n", lds_f, lds_i, S, rep, per,
+      printf("{\"pattern\": \"the step, one graph per stream\", \"lds_fwd\": %d, \"lds_inv\": %d, \"stagger\": %lld, "
+             "\"streams\": %d, \"rep\": %d, \"ms_per_step\": %.4f, \"Msamples_per_s\": %.1f, \"GBps\": %.1f}\n", lds_f,
+             lds_i, pstr - plane, S, rep, per,
              plane / (per * 1e-3) / 1e6, step_bytes / (per * 1e-3) / 1e9);
       fflush(stdout);
     }
     for (auto& x : ex) CHK(hipGraphExecDestroy(x));
   };
   for (int S : {1, 2, 4, 8}) run_graph(S);
-  if (argc > 2) return 0;
+  if (argc > 2 && argc <= 4) return 0;
   for (int S : {1, smax}) {
     run("fwd sc1 stores + inv nt (the step)", S, [&](const Set& s, long long rows, long long r0, hipStream_t q) {
-      hipLaunchKernelGGL(fanout<16>, dim3((unsigned)rows), dim3(512), 0, q, s.x, s.c, N, plane, J, r0);
+      hipLaunchKernelGGL(fanout<16>, dim3((unsigned)rows), dim3(512), 0, q, s.x, s.c, N, pstr, J, r0);
     });
     run("fwd nt stores + inv nt", S, [&](const Set& s, long long rows, long long r0, hipStream_t q) {
-      hipLaunchKernelGGL(fanout<-1>, dim3((unsigned)rows), dim3(512), 0, q, s.x, s.c, N, plane, J, r0);
+      hipLaunchKernelGGL(fanout<-1>, dim3((unsigned)rows), dim3(512), 0, q, s.x, s.c, N, pstr, J, r0);
     });
     run("fwd write-back stores + inv nt", S, [&](const Set& s, long long rows, long long r0, hipStream_t q) {
-      hipLaunchKernelGGL(fanout<0>, dim3((unsigned)rows), dim3(512), 0, q, s.x, s.c, N, plane, J, r0);
+      hipLaunchKernelGGL(fanout<0>, dim3((unsigned)rows), dim3(512), 0, q, s.x, s.c, N, pstr, J, r0);
     });
   }
   // each pass alone (1 stream, rotated sets): the forward pattern, then the inverse pattern
   for (int pass = 0; pass < 2; ++pass) {
     for (int i = 0; i < WARM; ++i) {
       const Set& s = sets[i % R];
-      if (pass == 0) hipLaunchKernelGGL(fanout<16>, dim3(B), dim3(512), 0, st[0], s.x, s.c, N, plane, J, 0LL);
-      else hipLaunchKernelGGL(fanin, dim3(B), dim3(512), 0, st[0], s.c, s.y, N, plane, J, 0LL);
+      if (pass == 0) hipLaunchKernelGGL(fanout<16>, dim3(B), dim3(512), 0, st[0], s.x, s.c, N, pstr, J, 0LL);
+      else hipLaunchKernelGGL(fanin, dim3(B), dim3(512), 0, st[0], s.c, s.y, N, pstr, J, 0LL);
     }
     CHK(hipEventRecord(e0, st[0]));
     for (int i = 0; i < K; ++i) {
       const Set& s = sets[i % R];
-      if (pass == 0) hipLaunchKernelGGL(fanout<16>, dim3(B), dim3(512), 0, st[0], s.x, s.c, N, plane, J, 0LL);
-      else hipLaunchKernelGGL(fanin, dim3(B), dim3(512), 0, st[0], s.c, s.y, N, plane, J, 0LL);
+      if (pass == 0) hipLaunchKernelGGL(fanout<16>, dim3(B), dim3(512), 0, st[0], s.x, s.c, N, pstr, J, 0LL);
+      else hipLaunchKernelGGL(fanin, dim3(B), dim3(512), 0, st[0], s.c, s.y, N, pstr, J, 0LL);
     }
     CHK(hipEventRecord(e1, st[0]));
     CHK(hipEventSynchronize(e1));
