@@ -132,7 +132,10 @@ enum {
      * :210-335, :435-487).  With this flag every row that holds a non-finite value in the call's inputs or
      * outputs is recomputed with the reference's full-tap loops (exact arithmetic, also under
      * VW_FLAG_FMA): NaN and +-Inf land exactly where the reference puts them.  Costs one extra read of
-     * the call's planes; streaming (vw_stream_*) ZERO / SYMMETRIC blocks are not covered. */
+     * the call's planes (none where the kernel probes its own rows) and one fix-up launch.  Streaming
+     * (vw_stream_*) ZERO / SYMMETRIC blocks and flushes are covered too: the history convolution
+     * (BatchSIMDMODWT.generalBatchMODWTSoAWithScaledFiltersAndHistory :447-507) multiplies every tap, and
+     * the recomputed rows rewrite the histories they leave for the next block. */
     VW_FLAG_REF_NONFINITE = 1u << 8
 };
 

@@ -634,7 +634,7 @@ JNIEXPORT jint JNICALL VW_JNI(streamFlushAoS)(JNIEnv *e, jclass c, jlong stream,
   int oom = 0;
   double *pd = out_buf(1, (size_t)J * n, &oom), *pa = out_buf(2, n, &oom);
   if (oom) return oom_error(e);
-  vw_status st = vw_stream_flush_f64(s, tailLength, HOST_FLAGS, pd, pa);
+  vw_status st = vw_stream_flush_f64(s, tailLength, HOST_FLAGS | VW_FLAG_REF_NONFINITE, pd, pa);
   for (jsize l = 0; l < J && st == VW_OK && tailLength > 0; ++l) {
     jobjectArray pl = plane(e, details, l);
     if (!scatter_rows(e, pl, 0, B, tailLength, pd + (size_t)l * n)) st = VW_ERR_ARG;

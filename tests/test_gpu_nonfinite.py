@@ -159,6 +159,37 @@ def test_swt_parallel_forward_inverse_nonfinite(engine, boundary):
         same(y[b], y_ref, f"inverse row {b}")
 
 
+@pytest.mark.parametrize("boundary", [O.ZERO_PADDING, O.SYMMETRIC], ids=["Z", "S"])
+@pytest.mark.parametrize("blk", [256, 16], ids=["blk256", "blk16-shorter-than-history"])
+def test_streaming_history_blocks_nonfinite(engine, boundary, blk):
+    # BatchStreamingMODWT ZERO / SYMMETRIC: the history convolution multiplies every upsampled tap
+    # (BatchSIMDMODWT.java:447-507), so a NaN / +-Inf spreads through the zero taps of this block AND, via
+    # the history it leaves, into later blocks; the recomputed rows rewrite their histories.  First
+    # block (history initialised from the block), later blocks, blocks shorter than the deepest history
+    # (carry), and the flush tail -- identity with the restatement for every row and block.
+    w, J, B = Daubechies.DB4, 4, 4
+    x = signals(B, blk * 4, 3)
+    x[0, 5] = np.nan                      # first block
+    x[1, blk + blk // 2] = np.inf         # second block
+    x[2, 3 * blk - 1] = -np.inf           # end of the third block: only the history carries it on
+    st = vw.BatchStreamingMODWT(w, vw.BoundaryMode(boundary), J)
+    refs = [O.StreamRestatement(*lohi(w), boundary, J) for _ in range(B)]
+    for k in range(4):
+        out = st.processMultiLevel(x[:, k * blk:(k + 1) * blk])
+        for b in range(B):
+            d_ref, a_ref = refs[b].process(x[b, k * blk:(k + 1) * blk])
+            same(out.detailPerLevel[:, b, :], d_ref, f"block {k} details row {b}")
+            same(out.finalApprox[b], a_ref, f"block {k} approx row {b}")
+    assert not np.isfinite(out.detailPerLevel[:, 2, :]).all()  # block 4 of row 2: only its history is poisoned
+    tl = st.getMinFlushTailLength()
+    tail = st.flushMultiLevel(tl)
+    for b in range(B):
+        d_ref, a_ref = refs[b].flush(tl)
+        same(tail.detailPerLevel[:, b, :], d_ref, f"flush details row {b}")
+        same(tail.finalApprox[b], a_ref, f"flush approx row {b}")
+    st.close()
+
+
 def test_streaming_periodic_blocks_nonfinite(engine):
     # BatchStreamingMODWT PERIODIC blocks are independent BatchMODWT blocks (BatchStreamingMODWT.java:110-116)
     w, n, J = Daubechies.DB4, 1024, 4

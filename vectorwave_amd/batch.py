@@ -240,8 +240,8 @@ class BatchStreamingMODWT:
         B, n = xa.shape
         det = self._engine._empty(xa, dev, (self.levels, B, n))
         app = self._engine._empty(xa, dev, (B, n))
-        # PERIODIC blocks are BatchMODWT blocks: the reference's NaN spread through the zero taps
-        # (ZERO / SYMMETRIC blocks with history are not covered by the flag, include/vectorwave_amd.h)
+        # the reference's NaN spread through the zero taps (BatchMODWT blocks for PERIODIC; for ZERO /
+        # SYMMETRIC the history-convolution loop, BatchSIMDMODWT.java:447-507, multiplies every tap too)
         fl = (0 if dev else nat.FLAG_HOST_MEMORY) | nat.FLAG_REF_NONFINITE
         _check(self._engine.lib.vw_stream_process_f64(self._h, xp, B, n, fl,
                                                       self._engine._ptr(det, dev), self._engine._ptr(app, dev)))
@@ -267,7 +267,7 @@ class BatchStreamingMODWT:
         B = self._last_batch()
         det = np.empty((self.levels, B, tailLength))
         app = np.empty((B, tailLength))
-        _check(self._engine.lib.vw_stream_flush_f64(self._h, tailLength, nat.FLAG_HOST_MEMORY,
+        _check(self._engine.lib.vw_stream_flush_f64(self._h, tailLength, nat.FLAG_HOST_MEMORY | nat.FLAG_REF_NONFINITE,
                                                     det.ctypes.data_as(c_void_p), app.ctypes.data_as(c_void_p)))
         return det, app
 

@@ -237,6 +237,7 @@ struct vw_stream {
   int64_t last_batch = -1;
   bool hist_init = false;
   std::vector<double*> hist;        // device [B][hist_len_j]
+  std::vector<double*> snap;        // VW_FLAG_REF_NONFINITE: the histories a block read (same shapes)
   std::vector<int> hist_len;
 };
 
@@ -1166,7 +1167,14 @@ static void deep_segments(const Tuning& tu, int cus, int64_t B, DeepArgs<T>* a) 
 // output), then recompute those rows with the reference's full-tap loops.  Stream-ordered, capturable
 // once the workspace has grown.
 template <typename T>
-static vw_status ref_nonfinite(vw_ctx* c, const std::vector<std::pair<const T*, int64_t>>& planes, RefArgs<T>& r,
+struct ScanPlane {
+  const T* p;
+  int64_t ld;
+  int len;  // 0: the call's N
+};
+
+template <typename T>
+static vw_status ref_nonfinite(vw_ctx* c, const std::vector<ScanPlane<T>>& planes, RefArgs<T>& r,
                                bool inverse, bool flagged) {
   const int64_t B = r.B, N = r.N;
   if ((int)planes.size() > kRefPlanes) return fail(VW_ERR_ARG, "too many planes for the non-finite scan");
@@ -1183,8 +1191,9 @@ static vw_status ref_nonfinite(vw_ctx* c, const std::vector<std::pair<const T*, 
     RefScan<T> s;
     memset(&s, 0, sizeof(s));
     for (const auto& p : planes) {
-      s.p[s.np] = p.first;
-      s.ld[s.np] = p.second;
+      s.p[s.np] = p.p;
+      s.ld[s.np] = p.ld;
+      s.len[s.np] = p.len;
       ++s.np;
     }
     s.B = B; s.N = (int)N; s.chunks = ref_scan_chunks((int)N); s.flag = c->nf;
@@ -1213,7 +1222,8 @@ static int ref_mode(int boundary) {
 template <typename T>
 static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64_t ldx, const double* lo,
                               const double* hi, int L, int boundary, int J, unsigned flags, T* details, T* approx,
-                              bool single_level, int mode_override, T* const* hist, bool hist_update) {
+                              bool single_level, int mode_override, T* const* hist, bool hist_update,
+                              T* const* hist_snap = nullptr, bool hist_first = false) {
   constexpr int V = vec_width<T>();
   VW_TRY(capture_guard(c, flags));
   const bool fma = flags & VW_FLAG_FMA;
@@ -1243,6 +1253,13 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     if (mode_override >= 0) d.mode = mode_override;
     max_hl = std::max(max_hl, d.hl);
   }
+  // VW_FLAG_REF_NONFINITE on a streaming block: keep the histories this block reads (the kernels
+  // overwrite them) for the rows vw_ref.hip recomputes
+  if ((flags & VW_FLAG_REF_NONFINITE) && hist && hist_update && hist_snap && !hist_first && J >= 2)
+    for (int j = 0; j < J; ++j)
+      if (lv[j].hist_len > 0)
+        VW_HIP(hipMemcpyAsync(hist_snap[j], hist[j], (size_t)B * lv[j].hist_len * sizeof(T), hipMemcpyDeviceToDevice,
+                              c->stream));
 
   const int hlpad = (int)round_up(max_hl, V);
   int threads = 0, lds = 0, nv = 4;
@@ -1257,9 +1274,10 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
   // or streaming history.  VW_FWD_PERSIST=0 disables it.
   const Tuning& tu = c->tune;
   const bool persist_on = tu.fwd_persist;
-  // the unvalidated callers' NaN spread through the zero taps (single level and J = 1 have none)
-  const bool ref_nf = (flags & VW_FLAG_REF_NONFINITE) && !validate && !single_level && !hist && J >= 2 &&
-                      !(flags & VW_FLAG_FFT_SWITCH);
+  // the unvalidated callers' NaN spread through the zero taps (single level and J = 1 have none); a
+  // streaming block that updates its history needs the snapshot of the histories it read (stream_run)
+  const bool ref_nf = (flags & VW_FLAG_REF_NONFINITE) && !validate && !single_level && J >= 2 &&
+                      !(flags & VW_FLAG_FFT_SWITCH) && (!hist || !hist_update || hist_first || hist_snap);
   bool nf_probed = false;
   const bool io_aligned = (ldx % V == 0) && (N % V == 0) && aligned16(x) && aligned16(details) && aligned16(approx);
   auto persist_ok = [&](int th, int nvv, bool ft) {
@@ -1484,14 +1502,25 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
   }
   if (ref_nf) {
     const size_t plane = (size_t)B * (size_t)N;
-    std::vector<std::pair<const T*, int64_t>> planes;
-    planes.push_back({x, ldx});
-    for (int j = 0; j < J; ++j) planes.push_back({details + j * plane, N});
-    planes.push_back({approx, N});
+    std::vector<ScanPlane<T>> planes;
+    planes.push_back({x, ldx, 0});
+    for (int j = 0; j < J; ++j) planes.push_back({details + j * plane, N, 0});
+    planes.push_back({approx, N, 0});
     RefArgs<T> r;
     memset(&r, 0, sizeof(r));
     r.x = x; r.ldx = ldx; r.details = details; r.approx = approx;
     r.B = B; r.N = (int)N; r.J = J; r.L = L; r.mode = ref_mode(boundary);
+    if (hist) {  // BatchStreamingMODWT block / flush: the histories the block read, and the ones it leaves
+      r.hist_mode = 1;
+      r.hist_first = hist_first ? 1 : 0;
+      for (int j = 0; j < J; ++j) {
+        const int hl = lv[j].hist_len;
+        r.hist_len[j] = hl;
+        r.hist_old[j] = hist_first ? nullptr : (hist_update ? hist_snap[j] : hist[j]);
+        r.hist_new[j] = hist_update ? hist[j] : nullptr;
+        if (r.hist_old[j] && hl > 0) planes.push_back({r.hist_old[j], hl, hl});
+      }
+    }
     copy_taps(r.lo, lo, L);
     copy_taps(r.hi, hi, L);
     VW_TRY(ref_nonfinite<T>(c, planes, r, false, nf_probed));
@@ -1834,11 +1863,11 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   }
   if (ref_nf) {
     const size_t plane = (size_t)B * (size_t)N;
-    std::vector<std::pair<const T*, int64_t>> planes;
+    std::vector<ScanPlane<T>> planes;
     for (int j = 0; j < J; ++j)
-      if (lv[j].use_d) planes.push_back({details + j * plane, N});
-    if (!approx_zero) planes.push_back({approx, N});
-    planes.push_back({y, N});
+      if (lv[j].use_d) planes.push_back({details + j * plane, N, 0});
+    if (!approx_zero) planes.push_back({approx, N, 0});
+    planes.push_back({y, N, 0});
     RefArgs<T> r;
     memset(&r, 0, sizeof(r));
     r.x = approx_zero ? nullptr : approx; r.det_in = details; r.y = y;
@@ -2626,6 +2655,7 @@ extern "C" vw_status vw_stream_create(vw_ctx* c, const double* lo, const double*
   s->boundary = boundary;
   s->levels = levels;
   s->hist.assign(levels, nullptr);
+  s->snap.assign(levels, nullptr);
   s->hist_len.resize(levels);
   for (int j = 1; j <= levels; ++j) s->hist_len[j - 1] = (int)(vw_upsampled_length(L, j) - 1);
   *out = s;
@@ -2633,10 +2663,11 @@ extern "C" vw_status vw_stream_create(vw_ctx* c, const double* lo, const double*
 }
 
 static void free_hist(vw_stream* s) {
-  for (auto& p : s->hist) {
-    if (p) hipFree(p);
-    p = nullptr;
-  }
+  for (auto* v : {&s->hist, &s->snap})
+    for (auto& p : *v) {
+      if (p) hipFree(p);
+      p = nullptr;
+    }
 }
 
 extern "C" vw_status vw_stream_destroy(vw_stream* s) {
@@ -2666,7 +2697,8 @@ static vw_status stream_run(vw_stream* s, const double* blk, int64_t B, int64_t 
   const bool first = !s->hist_init;
   const int mode = first ? -1 : kHaloHistory;
   return forward_impl<double>(c, blk, B, n, n, s->lo.data(), s->hi.data(), s->L, s->boundary, s->levels,
-                              flags & ~VW_FLAG_SYNC, details, approx, false, mode, s->hist.data(), !flush);
+                              flags & ~VW_FLAG_SYNC, details, approx, false, mode, s->hist.data(), !flush,
+                              s->snap[0] ? s->snap.data() : nullptr, first);
 }
 
 extern "C" vw_status vw_stream_process_f64(vw_stream* s, const double* block, int64_t B, int64_t n, unsigned flags,
@@ -2686,6 +2718,9 @@ extern "C" vw_status vw_stream_process_f64(vw_stream* s, const double* block, in
       s->hist_init = false;
       s->last_batch = B;
     }
+    if ((flags & VW_FLAG_REF_NONFINITE) && !s->snap[0])
+      for (int j = 0; j < s->levels; ++j)
+        VW_HIP(hipMalloc(&s->snap[j], std::max<size_t>((size_t)B * s->hist_len[j] * sizeof(double), 16)));
   }
   vw_status st;
   if (flags & VW_FLAG_HOST_MEMORY) {

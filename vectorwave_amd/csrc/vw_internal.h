@@ -184,11 +184,12 @@ struct DenoiseConsts {
 };
 
 // The reference's own arithmetic for rows holding non-finite values (vw_ref.hip, VW_FLAG_REF_NONFINITE).
-constexpr int kRefPlanes = kMaxLevels + 3;
+constexpr int kRefPlanes = 2 * kMaxLevels + 3;  // x, J details, approx, J streaming histories
 template <typename T>
 struct RefScan {                // flag[b] = 1 when row b of any plane is non-finite somewhere
   const T* p[kRefPlanes];
   long long ld[kRefPlanes];     // row stride of plane k
+  int len[kRefPlanes];          // row length of plane k (0: N)
   int np;
   long long B;
   int N;
@@ -211,6 +212,14 @@ struct RefArgs {
   int J;
   int L;
   int mode;                     // kHaloPeriodic / kHaloZero / kHaloSymmetric
+  // forward, BatchStreamingMODWT ZERO / SYMMETRIC blocks: samples left of the block come from the level's
+  // history (hist_old, [B][hist_len_j] oldest first; hist_first: the history the first block initialises,
+  // zeros / the mirror of the level input); hist_new (nullptr: none, e.g. a flush) receives the updated one
+  int hist_mode;
+  int hist_first;
+  const T* hist_old[kMaxLevels];
+  T* hist_new[kMaxLevels];
+  int hist_len[kMaxLevels];
   int* flag;                    // rows to recompute (cleared once recomputed)
   T* scratch;                   // [grid][2][N] running approximations
   T lo[kMaxTaps];               // base taps * 1/sqrt(2), as the fast kernels

@@ -63,7 +63,8 @@ __global__ void __launch_bounds__(kScanThreads) k_flag_nonfinite(RefScan<T> a) {
   bool bad = false;
   for (int p = 0; p < a.np; ++p) {
     const T* row = a.p[p] + b * a.ld[p];
-    for (int i = c0 + (int)threadIdx.x; i < c1; i += kScanThreads) bad |= !__builtin_isfinite(row[i]);
+    const int e = min(c1, a.len[p] ? a.len[p] : a.N);
+    for (int i = c0 + (int)threadIdx.x; i < e; i += kScanThreads) bad |= !__builtin_isfinite(row[i]);
   }
   // one store per wave that saw one (a plain vector store: every writer stores the same 1)
   if (__any(bad) && (threadIdx.x & 63) == 0) a.flag[b] = 1;
@@ -74,6 +75,10 @@ __global__ void __launch_bounds__(kScanThreads) k_flag_nonfinite(RefScan<T> a) {
 //             (t - l + N) % N wherever BatchSIMDMODWT can run, L_j <= N + 1)
 //   ZERO      terms with idx < 0 skipped                            convolveZeroPadChunk :303-318
 //   SYMMETRIC idx mirrored                                          convolveSymmetricChunk :321-335
+//   history   idx < 0 reads the level's history at hl + idx        BatchSIMDMODWT
+//             (BatchStreamingMODWT blocks)                          .generalBatchMODWTSoAWithScaledFiltersAndHistory
+//                                                                   :447-507; history initialised / updated as
+//                                                                   BatchStreamingMODWT :131-147, :326-352
 // a += f_lo[l] * x[idx], d += f_hi[l] * x[idx], l = 0 .. L_j - 1 ascending, f[l] = 0 off the 2^(j-1) grid.
 template <typename T>
 __global__ void __launch_bounds__(512) k_ref_forward(RefArgs<T> a) {
@@ -87,6 +92,13 @@ __global__ void __launch_bounds__(512) k_ref_forward(RefArgs<T> a) {
       const int s = 1 << (j - 1);
       T* out_a = (j == a.J) ? a.approx + b * (long long)N : ((j & 1) ? s0 : s1);
       T* out_d = a.details + ((size_t)(j - 1) * (size_t)a.B + (size_t)b) * (size_t)N;
+      const int hl = a.hist_mode ? a.hist_len[j - 1] : 0;
+      const T* ho = (a.hist_mode && !a.hist_first) ? a.hist_old[j - 1] + b * (long long)hl : nullptr;
+      // history position p (sample p - hl of the stream): the snapshot, or the one the first block creates
+      auto hist = [&](int p) -> T {
+        if (ho) return ho[p];
+        return a.mode == kHaloZero ? T(0) : cur[ref_sym(p - hl, N)];  // fillSymmetricHistoryFromSoA :326-335
+      };
       for (int t = threadIdx.x; t < N; t += blockDim.x) {
         T sa = T(0), sd = T(0);
         for (int i = 0; i < a.L; ++i) {
@@ -94,11 +106,16 @@ __global__ void __launch_bounds__(512) k_ref_forward(RefArgs<T> a) {
           for (int r = 0; r < reps; ++r) {
             const int l = i * s + r;
             int idx = t - l;
-            if (idx < 0) {
+            T v;
+            if (idx >= 0) {
+              v = cur[idx];
+            } else if (a.hist_mode) {
+              v = hist(hl + idx);
+            } else {
               if (a.mode == kHaloZero) continue;
               idx = a.mode == kHaloSymmetric ? ref_sym(idx, N) : ((idx % N) + N) % N;
+              v = cur[idx];
             }
-            const T v = cur[idx];
             const T fl = r == 0 ? a.lo[i] : T(0), fh = r == 0 ? a.hi[i] : T(0);
             sa = sa + fl * v;
             sd = sd + fh * v;
@@ -106,6 +123,13 @@ __global__ void __launch_bounds__(512) k_ref_forward(RefArgs<T> a) {
         }
         out_a[t] = sa;
         out_d[t] = sd;
+      }
+      // updateHistoryFromSoA :337-352: the last hl samples of the level input, or (n < hl) the old
+      // history shifted by n followed by the whole input
+      if (a.hist_mode && a.hist_new[j - 1]) {
+        T* hn = a.hist_new[j - 1] + b * (long long)hl;
+        for (int p = threadIdx.x; p < hl; p += blockDim.x)
+          hn[p] = N >= hl ? cur[N - hl + p] : (p < hl - N ? hist(p + N) : cur[p - (hl - N)]);
       }
       __syncthreads();  // the level's approximation is the next level's input (same workgroup, same CU)
       cur = out_a;
