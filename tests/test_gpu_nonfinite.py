@@ -137,6 +137,25 @@ def test_swt_denoise_parallel_branch_nonfinite_config3(engine, soft):
         same(y[b], y_ref, f"denoised row {b}")
 
 
+def test_config3_kernels_flag_their_own_rows(engine):
+    # config 3 runs the register-blocked kernels (k_forward_blk / k_inverse_blk), which probe their details /
+    # output in-line: no scan of the call's planes (timing family "ref_nonfinite", not "..._scan")
+    w, n, J = Symlet.SYM8, 16384, 8
+    x = poisoned(3, n, 7)
+    swt = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode.PERIODIC)
+    engine.enable_timing(True)
+    engine.reset_timing()
+    try:
+        y = swt.denoise(x, J)
+        assert engine.kernel_time("ref_nonfinite_scan")[1] == 0
+        assert engine.kernel_time("ref_nonfinite")[1] == 2
+    finally:
+        engine.enable_timing(False)
+    for b in range(3):
+        y_ref, _ = O.swt_denoise(x[b], *lohi(w), O.PERIODIC, J, soft=True, wavelet_id=w.wavelet_id)
+        same(y[b], y_ref, f"denoised row {b}")
+
+
 @pytest.mark.parametrize("boundary", [O.PERIODIC, O.SYMMETRIC, O.ZERO_PADDING], ids=["P", "S", "Z"])
 def test_swt_parallel_forward_inverse_nonfinite(engine, boundary):
     # forwardParallel's three chunk loops (:282-335) and the matching inverse (reconstructPeriodic, or core

@@ -1374,8 +1374,9 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
         mfma_lds = (int)((region + 2 * L + scratch) * 4);
       }
     }
-    // VW_FLAG_REF_NONFINITE: the persistent forward probes its own outputs (no scan pass afterwards)
-    if (ref_nf && persist && !mfma_lds && !blk_lds) {
+    // VW_FLAG_REF_NONFINITE: the persistent and the register-blocked forward probe their own details (no
+    // scan pass afterwards)
+    if (ref_nf && !mfma_lds && (blk_lds || persist)) {
       VW_TRY(ensure_nf(c, B));
       a.nf_flag = c->nf;
       nf_probed = true;
@@ -1668,10 +1669,9 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         mfma_lds = (int)((region + 2 * L) * 4);
       }
     }
-    // VW_FLAG_REF_NONFINITE: the one-buffer sequential kernel (vw_inv.hip's choice) probes its inputs and
-    // output itself (no scan pass afterwards)
-    const bool inv_blk = a.blk && a.unrolled && has_unrolled_taps(L) && nv != 2;
-    if (ref_nf && !mfma_lds && !a.pair && !a.db && !inv_blk) {
+    // VW_FLAG_REF_NONFINITE: the one-buffer sequential kernels (k_inverse_seq / k_inverse_blk, vw_inv.hip's
+    // choice) probe their output themselves (no scan pass afterwards)
+    if (ref_nf && !mfma_lds && !a.pair && !a.db) {
       VW_TRY(ensure_nf(c, B));
       a.nf_flag = c->nf;
       nf_probed = true;

@@ -1668,6 +1668,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
       __builtin_amdgcn_sched_barrier(0);
     }
   }
+  T nf = T(0);  // VW_FLAG_REF_NONFINITE: the details' probe (as k_forward_persist)
   for (int j = 1; j <= p.J; ++j) {
     const int m = m_of(j);
     lds_barrier();  // X = level input + images; every read of Y (previous level) done
@@ -1725,6 +1726,10 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
         fwd_row_t<T, L, FMA, NV, 1>(X + HLV * V, nvec, 1, flo, fhi, p.taps, em);
       }
     }
+    if (p.nf_flag) {
+#pragma unroll
+      for (int r = 0; r < NV; ++r) nf_probe<T, V>(nf, ah[r]);
+    }
     if (!last) {
       if (!dbl) lds_barrier();  // one buffer: every read of this level's input done first
 #pragma unroll
@@ -1740,6 +1745,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
       T* t = X; X = Y; Y = t;
     }
   }
+  if (p.nf_flag) nf_flag_row<T>(p.nf_flag, b, nf);
 }
 
 // Inverse, PERIODIC, sequential sums (K4), one region time-shared as k_inverse_seq.  Right wrap
@@ -1835,6 +1841,12 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 6)) k_inverse_blk(const InvArg
   // level 1 (s = 1 < V) ran in the standard mapping: coalesced stores
 #pragma unroll
   for (int k = 0; k < NV; ++k) store_vec<VW_INV_STORE_AUX>(p.y + b * (size_t)N, (tid + k * NT) * V, N, true, acc[k]);
+  if (p.nf_flag) {  // VW_FLAG_REF_NONFINITE: y's probe (as k_inverse_seq)
+    T nf = T(0);
+#pragma unroll
+    for (int k = 0; k < NV; ++k) nf_probe<T, V>(nf, acc[k]);
+    nf_flag_row<T>(p.nf_flag, b, nf);
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
