@@ -104,7 +104,7 @@ def parse(argv=None):
     p.add_argument("--ref-nonfinite", default="off", choices=["on", "off"],
                    help="VW_FLAG_REF_NONFINITE (the unvalidated batch facade's NaN/Inf spread, vw_ref.hip) on the "
                         "timed calls: identical results for finite data; db4's kernels probe their rows in-line "
-                        "and each pass adds one fix-up launch (-2.5 %%, profiles/r06/ab_db4_ref_nonfinite_on_off.log)")
+                        "and each pass adds one fix-up launch (-0.9 %% on db4, profiles/r06/ab_db4_ref_nonfinite_on_off_final_probe.log)")
     p.add_argument("--no-weak", action="store_true", help="N > 1: skip the weak-scaling measurement")
     p.add_argument("--launch", default="graph-k", choices=sorted(LAUNCH_DESC),
                    help="how the timed steps are issued (see measure())")

@@ -129,10 +129,11 @@ enum {
      * -- BatchMODWT.multiLevelAoS (ext/extensions/modwt/BatchSIMDMODWT.java:384-424),
      * inverseMultiLevelAoS -> MultiLevelMODWTTransform.reconstruct (core/modwt/MultiLevelMODWTTransform.java
      * :339-349, :554-645), VectorWaveSwtAdapter.forwardParallel / inverse (core/swt/VectorWaveSwtAdapter.java
-     * :210-335, :435-487).  With this flag every row that holds a non-finite value in the call's inputs or
-     * outputs is recomputed with the reference's full-tap loops (exact arithmetic, also under
-     * VW_FLAG_FMA): NaN and +-Inf land exactly where the reference puts them.  Costs one extra read of
-     * the call's planes (none where the kernel probes its own rows) and one fix-up launch.  Streaming
+     * :210-335, :435-487).  With this flag every row where a level input holds a non-finite value (found
+     * on the cascade's final output, a_J / y, which every such value reaches) is recomputed with the
+     * reference's full-tap loops (exact arithmetic, also under VW_FLAG_FMA): NaN and +-Inf land exactly
+     * where the reference puts them.  Costs one read of that output plane (none where the kernel probes
+     * its own rows) and one fix-up launch.  Streaming
      * (vw_stream_*) ZERO / SYMMETRIC blocks and flushes are covered too: the history convolution
      * (BatchSIMDMODWT.generalBatchMODWTSoAWithScaledFiltersAndHistory :447-507) multiplies every tap, and
      * the recomputed rows rewrite the histories they leave for the next block. */

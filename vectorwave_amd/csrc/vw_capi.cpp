@@ -1374,8 +1374,8 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
         mfma_lds = (int)((region + 2 * L + scratch) * 4);
       }
     }
-    // VW_FLAG_REF_NONFINITE: the persistent and the register-blocked forward probe their own details (no
-    // scan pass afterwards)
+    // VW_FLAG_REF_NONFINITE: the persistent and the register-blocked forward probe their a_J (no scan pass
+    // afterwards)
     if (ref_nf && !mfma_lds && (blk_lds || persist)) {
       VW_TRY(ensure_nf(c, B));
       a.nf_flag = c->nf;
@@ -1503,10 +1503,9 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
   }
   if (ref_nf) {
     const size_t plane = (size_t)B * (size_t)N;
-    std::vector<ScanPlane<T>> planes;
-    planes.push_back({x, ldx, 0});
-    for (int j = 0; j < J; ++j) planes.push_back({details + j * plane, N, 0});
-    planes.push_back({approx, N, 0});
+    (void)plane;
+    // a_J alone: every non-finite level input (x, a_1 .. a_{J-1}, a history) reaches it (vw_ref.hip)
+    std::vector<ScanPlane<T>> planes{{approx, N, 0}};
     RefArgs<T> r;
     memset(&r, 0, sizeof(r));
     r.x = x; r.ldx = ldx; r.details = details; r.approx = approx;
@@ -1519,7 +1518,6 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
         r.hist_len[j] = hl;
         r.hist_old[j] = hist_first ? nullptr : (hist_update ? hist_snap[j] : hist[j]);
         r.hist_new[j] = hist_update ? hist[j] : nullptr;
-        if (r.hist_old[j] && hl > 0) planes.push_back({r.hist_old[j], hl, hl});
       }
     }
     copy_taps(r.lo, lo, L);
@@ -1863,11 +1861,9 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
   }
   if (ref_nf) {
     const size_t plane = (size_t)B * (size_t)N;
-    std::vector<ScanPlane<T>> planes;
-    for (int j = 0; j < J; ++j)
-      if (lv[j].use_d) planes.push_back({details + j * plane, N, 0});
-    if (!approx_zero) planes.push_back({approx, N, 0});
-    planes.push_back({y, N, 0});
+    (void)plane;
+    // y alone: every non-finite level input (a_J, a kept d_j, an intermediate approximation) reaches it
+    std::vector<ScanPlane<T>> planes{{y, N, 0}};
     RefArgs<T> r;
     memset(&r, 0, sizeof(r));
     r.x = approx_zero ? nullptr : approx; r.det_in = details; r.y = y;

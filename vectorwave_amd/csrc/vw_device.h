@@ -749,7 +749,7 @@ __device__ __forceinline__ void nf_flag_row(int* flag, long long b, T z) {
   if (__any(z != z) && (threadIdx.x & 63) == 0) flag[b] = 1;
 }
 
-// NFP: probe the details (nf: the row's accumulator, see nf_probe)
+// NFP: probe the final approximation (nf: the row's accumulator, see nf_probe)
 template <typename T, int L, bool FMA, int NV, bool VALIDATE, bool NFP = false>
 __device__ __forceinline__ void fwd_level(const FwdArgs<T>& p, const T* X, int nvec, const LevelDesc& lv, T* dout,
                                           T* aout, bool vec_ok, unsigned long long flat0, T (&areg)[NV][VT<T>::V],
@@ -764,7 +764,9 @@ __device__ __forceinline__ void fwd_level(const FwdArgs<T>& p, const T* X, int n
       check_out<T>(1, p.bad, flat0, t0, N, ah);
       check_out<T>(1, p.bad, flat0, t0, N, al);
     }
-    if constexpr (NFP) nf_probe<T, V>(*nf, ah);  // the details suffice (k_forward_persist)
+    if constexpr (NFP) {
+      if (aout) nf_probe<T, V>(*nf, al);  // a_J suffices (k_forward_persist; vw_ref.hip)
+    }
 #pragma unroll
     for (int e = 0; e < V; ++e) areg[k][e] = al[e];
   });
@@ -996,10 +998,7 @@ k_forward_persist(const FwdArgs<T> p) {
         T* t = X; X = Y; Y = t;
       }
     }
-    // VW_FLAG_REF_NONFINITE: the reference differs only where a level input (x, a_1 .. a_{J-1}) holds a
-    // NaN / +-Inf; such a value reaches that level's details through the non-zero high-pass taps (and a
-    // non-finite a_J is identical in both), so probing the details flags exactly the rows vw_ref.hip must
-    // recompute (an overflow to Inf in a detail sum adds a harmless recompute)
+    // VW_FLAG_REF_NONFINITE: probing a_J flags every row vw_ref.hip must recompute (see there)
     if (p.nf_flag) {
       nf_flag_row<T>(p.nf_flag, b, nf);
       nf = T(0);
@@ -1139,9 +1138,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, VW_INV_W)) k_inverse_seq(const
 
   T acc[NV][V];
   T dreg[NV][V];
-  // VW_FLAG_REF_NONFINITE: a NaN / +-Inf in any level input (a_J, a d_j the threshold keeps, an
-  // intermediate approximation) reaches y through the non-zero taps (0 * Inf never occurs in these sums),
-  // so probing y flags exactly the rows vw_ref.hip must recompute
+  // VW_FLAG_REF_NONFINITE: probing y flags every row vw_ref.hip must recompute (see there)
   T nf = T(0);
   const bool nfp = p.nf_flag != nullptr;
   load_row_regs<T, NV>(acc, p.approx + b * (size_t)N, N, nvec, vec_ok, p.approx_zero != 0);
@@ -1668,7 +1665,7 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
       __builtin_amdgcn_sched_barrier(0);
     }
   }
-  T nf = T(0);  // VW_FLAG_REF_NONFINITE: the details' probe (as k_forward_persist)
+  T nf = T(0);  // VW_FLAG_REF_NONFINITE: a_J's probe (as k_forward_persist)
   for (int j = 1; j <= p.J; ++j) {
     const int m = m_of(j);
     lds_barrier();  // X = level input + images; every read of Y (previous level) done
@@ -1726,9 +1723,9 @@ __global__ void VW_FUSED_BOUNDS(NV, VW_FUSED_W(L, 8)) k_forward_blk(const FwdArg
         fwd_row_t<T, L, FMA, NV, 1>(X + HLV * V, nvec, 1, flo, fhi, p.taps, em);
       }
     }
-    if (p.nf_flag) {
+    if (p.nf_flag && last) {
 #pragma unroll
-      for (int r = 0; r < NV; ++r) nf_probe<T, V>(nf, ah[r]);
+      for (int r = 0; r < NV; ++r) nf_probe<T, V>(nf, al[r]);
     }
     if (!last) {
       if (!dbl) lds_barrier();  // one buffer: every read of this level's input done first

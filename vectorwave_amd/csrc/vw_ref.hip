@@ -12,16 +12,19 @@
 //   VectorWaveSwtAdapter.forwardParallel  core/swt/VectorWaveSwtAdapter.java:210-335 (N >= 4096, J > 2)
 //   VectorWaveSwtAdapter.inverse / reconstructPeriodic  :435-487, and core reconstruct K5 / K6 :590-642
 // -- a non-finite sample turns every output whose window reaches it through a zero tap into NaN.
-// The engine keeps its fast kernels for every row and then, for the rows that hold a non-finite value
-// (flagged by k_flag_nonfinite over the call's inputs AND outputs, so an overflow to Inf inside the
-// cascade is caught too), recomputes the whole cascade here with the reference's loops: every tap,
-// zeros included, separate multiply and add in the reference's order -- bit-identical to it, NaN and
-// +-Inf included.  Flagged rows are rare (they are invalid input to every validated entry point), so
-// this is one persistent launch of one workgroup per row, reading the level input from global memory
-// (L2); a call with no flagged row pays one scan of its planes and an empty launch.  The headline
-// kernels (k_forward_persist, k_inverse_seq) flag their rows themselves (FwdArgs / InvArgs nf_flag: one
-// FMA per value, v * 0 + z is NaN iff v is not finite) and the scan is skipped.  Flags stay zero
-// between calls: these kernels clear every row they recompute.
+// The engine keeps its fast kernels for every row and then recomputes, with the reference's loops
+// (every tap, zeros included, separate multiply and add in the reference's order: bit-identical to it,
+// NaN and +-Inf included), exactly the rows whose results can differ: those where some level input --
+// x or an intermediate approximation in the forward; a_J, a kept d_j or an intermediate approximation in
+// the inverse; a streaming history -- holds a NaN / +-Inf.  Such a value reaches the final output of the
+// cascade through the non-zero taps (every filter's end taps are non-zero, and a sum with a non-finite
+// term never turns finite), so one look at the final output finds them: a_J of the forward, y of the
+// inverse -- in registers by the kernels that write it (FwdArgs / InvArgs nf_flag: v * 0 + z is NaN iff
+// v is not finite, one FMA per value), else by k_flag_nonfinite over that one plane.  (A finite row that
+// overflows to Inf there is recomputed too: harmless.)  Flagged rows are rare (they are invalid input to
+// every validated entry point), so the fix-up is one persistent launch of one workgroup per row, reading
+// the level input from global memory (L2).  Flags stay zero between calls: these kernels clear every row
+// they recompute.
 #include <hip/hip_runtime.h>
 #include "vw_internal.h"
 
