@@ -388,3 +388,39 @@ def test_swt_full_batch_rows_probe_themselves(engine, boundary):
             y_ref = O.reconstruct(d_ref, a_ref, w.lowPassReconstruction(), w.highPassReconstruction(), boundary,
                                   wavelet_id=w.wavelet_id)
         same(y[b], y_ref, f"inverse row {b}")
+
+
+def test_long_rows_probe_their_final_output(engine):
+    # config 4's row shape (db8 J = 10, 2^20 samples): multi-level tiles + the deep forward launch, chained
+    # column sweeps + multi-level inverse tiles.  The launches that write a_J / y probe it in registers (no
+    # scan of the plane); the poisoned row is the reference's bits, the clean one the fast kernels' bits.
+    import torch
+    from vectorwave_amd import _native as nat
+    from vectorwave_amd.wavelets import Daubechies as D
+    w, n, J, B = D.DB8, 1 << 20, 10, 2
+    x = O.fill_uniform(B * n, 5).reshape(B, n)
+    x[1, 777] = np.nan
+    lo, hi = lohi(w)
+    lr, hr = w.lowPassReconstruction(), w.highPassReconstruction()
+    xt = torch.from_numpy(x).cuda()
+    R = nat.FLAG_REF_NONFINITE
+    engine.enable_timing(True)
+    engine.reset_timing()
+    try:
+        d1, a1 = engine.forward(xt, lo, hi, w.wavelet_id, O.PERIODIC, J, R)
+        y1 = engine.inverse(d1, a1, lr, hr, w.wavelet_id, O.PERIODIC, J, R)
+        torch.cuda.synchronize()
+        scans = engine.kernel_time("ref_nonfinite_scan")[1]
+        probed = engine.kernel_time("ref_nonfinite")[1]
+    finally:
+        engine.enable_timing(False)
+    assert (probed, scans) == (2, 0), (probed, scans)
+    d0, a0 = engine.forward(xt, lo, hi, w.wavelet_id, O.PERIODIC, J, 0)
+    y0 = engine.inverse(d0, a0, lr, hr, w.wavelet_id, O.PERIODIC, J, 0)
+    d1, a1, y1 = d1.cpu().numpy(), a1.cpu().numpy(), y1.cpu().numpy()
+    assert np.array_equal(d1[:, 0].view(np.int64), d0[:, 0].cpu().numpy().view(np.int64))
+    assert np.array_equal(y1[0].view(np.int64), y0[0].cpu().numpy().view(np.int64))
+    d_ref, a_ref = O.decompose(x[1], lo, hi, O.PERIODIC, J, core=False)
+    same(d1[:, 1, :], d_ref, "details row 1")
+    same(a1[1], a_ref, "approx row 1")
+    same(y1[1], O.reconstruct(d_ref, a_ref, lr, hr, O.PERIODIC), "inverse row 1")

@@ -1417,6 +1417,11 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
         deep_segments<T>(tu, c->cus, B, &d);
         d.src = src; d.lda = lda; d.B = B; d.taps = L;
         d.out = (je == J) ? approx : nxt;
+        if (ref_nf && je == J) {  // the deep launch writes a_J: it probes it (VW_FLAG_REF_NONFINITE)
+          VW_TRY(ensure_nf(c, B));
+          d.nf_flag = c->nf;
+          nf_probed = true;
+        }
         for (int k = 0; k < d.g; ++k) d.out_d[k] = details + (size_t)(j - 1 + k) * plane;
         copy_taps(d.lo, lo, L);
         copy_taps(d.hi, hi, L);
@@ -1734,6 +1739,11 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
         memset(&m, 0, sizeof(m));
         m.src_a = cur;
         m.out_a = (j0 == 1) ? y : nxt;
+        if (ref_nf && j0 == 1) {  // the group writes y: it probes it (VW_FLAG_REF_NONFINITE)
+          VW_TRY(ensure_nf(c, B));
+          m.nf_flag = c->nf;
+          nf_probed = true;
+        }
         bool al = aligned16(cur) && aligned16(m.out_a);
         for (int k = 0; k < g; ++k) {
           const LevelDesc& d = lv[j0 - 1 + k];

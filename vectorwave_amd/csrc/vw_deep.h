@@ -17,6 +17,7 @@ struct DeepArgs {
   const T* src_d[kMaxGroup]; // inverse: d of level j0+k (nullptr = masked / zero)
   const T* thr[kMaxGroup];   // inverse denoise: thresholds [B] of level j0+k (nullptr = none)
   T* out;                    // forward: approximation of level j0+g-1; inverse: a_{j0-1}
+  int* nf_flag;              // forward, VW_FLAG_REF_NONFINITE, out = a_J: a_J's probe (nullptr = off)
   long long B;
   int N, P, C, nq, nb;       // nq = N / P decimated positions, nb = P / C residue blocks
   int g;                     // levels in the group

@@ -141,6 +141,7 @@ __global__ void __launch_bounds__(kDeepThreads) k_forward_deep(const DeepArgs<T>
   const int wave = tid >> 6, lane = tid & 63;
   const long long rowoff = wk.b * (long long)p.N + (long long)wk.rb * C;
   const T* __restrict__ src = p.src + wk.b * p.lda + (long long)wk.rb * C;
+  T nf = T(0);  // VW_FLAG_REF_NONFINITE (p.nf_flag: out = a_J): the probe of the stored approximation
   const int qs = wk.sg * p.seglen;
   const int qe = min(qs + p.seglen, nq);
   const int total = p.warm + (qe - qs);     // positions streamed
@@ -315,6 +316,9 @@ __global__ void __launch_bounds__(kDeepThreads) k_forward_deep(const DeepArgs<T>
             *reinterpret_cast<vec*>(lds + p.off[k + 1] + (v >= cap1 ? v - cap1 : v) * C + ce) = oa;
           } else if (live) {
             deep_store<vec>(p.out + gofs, oa);
+            if (p.nf_flag)
+#pragma unroll
+              for (int e = 0; e < V; ++e) nf = nf_step<T>(oa[e], nf);
           }
         }
       };
@@ -331,6 +335,7 @@ __global__ void __launch_bounds__(kDeepThreads) k_forward_deep(const DeepArgs<T>
     if (t + 1 < nt) wait_vmcnt_rt(pf.after(t + 1, t));
     lds_barrier();
   }
+  if (p.nf_flag) nf_flag_row<T>(p.nf_flag, wk.b, nf);
 }
 
 // ---------------------------------------------------------------------------------------------------

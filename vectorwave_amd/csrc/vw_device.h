@@ -730,13 +730,15 @@ __device__ __forceinline__ void zero_regs(T (&r)[NV][VT<T>::V]) {
 // ONE workgroup barrier.  With one buffer (long signals), a second barrier guards the overwrite.
 // Non-finite probe (VW_FLAG_REF_NONFINITE, vw_ref.hip): z = v * 0 + z stays +-0 while every v is finite
 // and becomes NaN for good at the first NaN / +-Inf -- one FMA per value, no compare or mask in the loop.
+template <typename T>
+__device__ __forceinline__ T nf_step(T v, T z) {
+  if constexpr (sizeof(T) == 8) return __builtin_fma(v, T(0), z);
+  else return __builtin_fmaf(v, T(0), z);
+}
 template <typename T, int V>
 __device__ __forceinline__ void nf_probe(T& z, const T (&v)[V]) {
 #pragma unroll
-  for (int e = 0; e < V; ++e) {
-    if constexpr (sizeof(T) == 8) z = __builtin_fma(v[e], T(0), z);
-    else z = __builtin_fmaf(v[e], T(0), z);
-  }
+  for (int e = 0; e < V; ++e) z = nf_step<T>(v[e], z);
 }
 // a row in registers (load_row_regs layout): only the vectors the thread holds (for_vecs)
 template <typename T, int L, int NV, int V>
@@ -2453,6 +2455,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
   const int span = (cnt + V - 1) / V * V;
   const bool vec_ok = p.vec_io != 0;
   const int top = p.nlev - 1;
+  T nf = T(0);  // VW_FLAG_REF_NONFINITE (p.nf_flag: the group ends at level 1): y's probe
   // Detail prefetch (p.pf, host contract: whole vectors, (span + ext[top]) / V <= kMultiPF * 256): the
   // tile of d_{k-1} is loaded into registers right after level k's first barrier and written to D
   // after its second, so the HBM latency of the next level's input overlaps this level's arithmetic.
@@ -2644,7 +2647,13 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
           if (k == 0) {
 #pragma unroll
             for (int r = 0; r < NI; ++r)
-              if (vb + m * r < nv) store_vec(p.out_a + b * (size_t)N + ts, (vb + m * r) * V, cnt, vec_ok, acc[r]);
+              if (vb + m * r < nv) {
+                store_vec(p.out_a + b * (size_t)N + ts, (vb + m * r) * V, cnt, vec_ok, acc[r]);
+                if (p.nf_flag)
+#pragma unroll
+                  for (int e = 0; e < V; ++e)
+                    if ((vb + m * r) * V + e < cnt) nf = nf_step<T>(acc[r][e], nf);
+              }
           }
         }
         if (k == 0) break;
@@ -2673,7 +2682,13 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
         // K4: all approximation taps, then all detail taps, into one accumulator
         inv_branch<T, L, FMA>(A, w * V, s, 1, 0, p.lo, p.taps, acc[i]);
         inv_branch<T, L, FMA>(D, w * V, s, 1, 0, p.hi, p.taps, acc[i]);
-        if (k == 0) store_vec(p.out_a + b * (size_t)N + ts, w * V, cnt, vec_ok, acc[i]);
+        if (k == 0) {
+          store_vec(p.out_a + b * (size_t)N + ts, w * V, cnt, vec_ok, acc[i]);
+          if (p.nf_flag)
+#pragma unroll
+            for (int e = 0; e < V; ++e)
+              if (w * V + e < cnt) nf = nf_step<T>(acc[i][e], nf);
+        }
       }
       __builtin_amdgcn_sched_barrier(0);  // one vector's LDS reads in flight at a time (VGPR budget)
     }
@@ -2692,6 +2707,7 @@ __global__ void __launch_bounds__(256) k_inverse_multi(const MultiArgs<T> p) {
     }
     if (pf) d_store(k - 1);
   }
+  if (p.nf_flag) nf_flag_row<T>(p.nf_flag, b, nf);  // VW_FLAG_REF_NONFINITE: y's probe (vw_ref.hip)
 }
 
 template <typename T>

@@ -164,6 +164,7 @@ struct MultiArgs {
   int rblk;                  // inverse: register-blocked taps where S is a multiple of V
   int pf;                    // inverse: next level's detail tile prefetched into registers
   int pad;                   // inverse: padded LDS layout at the register-blocked levels (needs pf, rblk)
+  int* nf_flag;              // inverse, VW_FLAG_REF_NONFINITE, the group writes y: y's probe (nullptr = off)
   int slack;                 // inverse: LDS vectors allocated past D (compile-time-stride reads, 0 = off)
   int ni;                    // inverse: output vectors per thread, kMultiInvNI or 4 (fp64)
   T lo[kMaxTaps];
