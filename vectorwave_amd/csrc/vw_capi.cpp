@@ -1507,8 +1507,6 @@ static vw_status forward_impl(vw_ctx* c, const T* x, int64_t B, int64_t N, int64
     }
   }
   if (ref_nf) {
-    const size_t plane = (size_t)B * (size_t)N;
-    (void)plane;
     // a_J alone: every non-finite level input (x, a_1 .. a_{J-1}, a history) reaches it (vw_ref.hip)
     std::vector<ScanPlane<T>> planes{{approx, N, 0}};
     RefArgs<T> r;
@@ -1870,8 +1868,6 @@ static vw_status inverse_impl(vw_ctx* c, const T* details, const T* approx, int6
     }
   }
   if (ref_nf) {
-    const size_t plane = (size_t)B * (size_t)N;
-    (void)plane;
     // y alone: every non-finite level input (a_J, a kept d_j, an intermediate approximation) reaches it
     std::vector<ScanPlane<T>> planes{{y, N, 0}};
     RefArgs<T> r;
