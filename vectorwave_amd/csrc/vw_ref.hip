@@ -11,6 +11,8 @@
 //   BatchMODWT.inverseMultiLevelAoS -> MultiLevelMODWTTransform.reconstruct (K4, :339-349, :576-589)
 //   VectorWaveSwtAdapter.forwardParallel  core/swt/VectorWaveSwtAdapter.java:210-335 (N >= 4096, J > 2)
 //   VectorWaveSwtAdapter.inverse / reconstructPeriodic  :435-487, and core reconstruct K5 / K6 :590-642
+//   BatchStreamingMODWT ZERO / SYMMETRIC blocks -> BatchSIMDMODWT
+//                                 .generalBatchMODWTSoAWithScaledFiltersAndHistory :447-507 (and its flush)
 // -- a non-finite sample turns every output whose window reaches it through a zero tap into NaN.
 // The engine keeps its fast kernels for every row and then recomputes, with the reference's loops
 // (every tap, zeros included, separate multiply and add in the reference's order: bit-identical to it,
