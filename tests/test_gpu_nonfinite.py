@@ -137,6 +137,24 @@ def test_swt_denoise_parallel_branch_nonfinite_config3(engine, soft):
         same(y[b], y_ref, f"denoised row {b}")
 
 
+@pytest.mark.parametrize("boundary", [O.SYMMETRIC, O.ZERO_PADDING], ids=["S", "Z"])
+@pytest.mark.parametrize("soft", [True, False], ids=["soft", "hard"])
+def test_swt_denoise_nonperiodic_nonfinite(engine, boundary, soft):
+    # the parallel branch on the other boundaries: forward convolution chunks (:303-335), universal
+    # thresholds, core reconstruct K5 / K6 -- 64 rows so the sequential inverse probes its output
+    w, n, J, B = Symlet.SYM8, 4096, 4, 64
+    x = O.fill_uniform(B * n, 29).reshape(B, n)
+    x[0, 0] = np.nan
+    x[31, 2000] = np.inf
+    x[B - 1, n - 1] = -np.inf
+    swt = vw.VectorWaveSwtAdapter(w, vw.BoundaryMode(boundary))
+    y, thr = swt.denoise(x, J, soft=soft, return_thresholds=True)
+    for b in (0, 1, 31, B - 1):
+        y_ref, t_ref = O.swt_denoise(x[b], *lohi(w), boundary, J, soft=soft, wavelet_id=w.wavelet_id)
+        same(thr[b], t_ref, f"threshold row {b}")
+        same(y[b], y_ref, f"denoised row {b}")
+
+
 def test_config3_kernels_flag_their_own_rows(engine):
     # config 3 runs the register-blocked kernels (k_forward_blk / k_inverse_blk), which probe their details /
     # output in-line: no scan of the call's planes (timing family "ref_nonfinite", not "..._scan")
