@@ -408,7 +408,8 @@ def test_swt_full_batch_rows_probe_themselves(engine, boundary):
         same(y[b], y_ref, f"inverse row {b}")
 
 
-def test_long_rows_probe_their_final_output(engine):
+@pytest.mark.parametrize("fma", [False, True], ids=["exact", "fma"])
+def test_long_rows_probe_their_final_output(engine, fma):
     # config 4's row shape (db8 J = 10, 2^20 samples): multi-level tiles + the deep forward launch, chained
     # column sweeps + multi-level inverse tiles.  The launches that write a_J / y probe it in registers (no
     # scan of the plane); the poisoned row is the reference's bits, the clean one the fast kernels' bits.
@@ -421,7 +422,8 @@ def test_long_rows_probe_their_final_output(engine):
     lo, hi = lohi(w)
     lr, hr = w.lowPassReconstruction(), w.highPassReconstruction()
     xt = torch.from_numpy(x).cuda()
-    R = nat.FLAG_REF_NONFINITE
+    F = nat.FLAG_FMA if fma else 0
+    R = nat.FLAG_REF_NONFINITE | F
     engine.enable_timing(True)
     engine.reset_timing()
     try:
@@ -433,8 +435,8 @@ def test_long_rows_probe_their_final_output(engine):
     finally:
         engine.enable_timing(False)
     assert (probed, scans) == (2, 0), (probed, scans)
-    d0, a0 = engine.forward(xt, lo, hi, w.wavelet_id, O.PERIODIC, J, 0)
-    y0 = engine.inverse(d0, a0, lr, hr, w.wavelet_id, O.PERIODIC, J, 0)
+    d0, a0 = engine.forward(xt, lo, hi, w.wavelet_id, O.PERIODIC, J, F)
+    y0 = engine.inverse(d0, a0, lr, hr, w.wavelet_id, O.PERIODIC, J, F)
     d1, a1, y1 = d1.cpu().numpy(), a1.cpu().numpy(), y1.cpu().numpy()
     assert np.array_equal(d1[:, 0].view(np.int64), d0[:, 0].cpu().numpy().view(np.int64))
     assert np.array_equal(y1[0].view(np.int64), y0[0].cpu().numpy().view(np.int64))
